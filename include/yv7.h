@@ -1,0 +1,130 @@
+/* yv7.h — C ABI of the MI355X-native YOLOv7 inference path (libyv7.so, gfx950).
+ *
+ * Plain C types only: every tensor crosses the boundary as a device pointer plus sizes; streams
+ * cross as hipStream_t passed as void*.  Every call returns 0 on success, a positive hipError_t
+ * on a HIP failure, or a negative yv7_status on an argument / shape error; the message is in the
+ * thread-local yv7_last_error().  Nothing throws or aborts across the ABI.  The caller owns every
+ * input, output and workspace buffer; a plan owns only its packed weights and small tables.
+ *
+ * What each entry point replaces in the reference (qbxlvnf11/yolo-series):
+ *   yv7_plan_create   attempt_load() -> Model.fuse() product   models/experimental.py:247-270,
+ *                     models/yolo.py:693-710 (the fused, deploy-form network: weights folded on the
+ *                     host by the Python mirror, packed NHWC/KRSC and handed over here once)
+ *   yv7_forward       Model.forward / forward_once            models/yolo.py:581-631, including every
+ *                     layer forward (Conv.fuseforward common.py:110-111, RepConv common.py:498-500,
+ *                     SPPCSPC common.py:276-280, MP/SP common.py:30-45, ReOrg common.py:48-53,
+ *                     Concat common.py:56-62, nn.Upsample) and Detect/IDetect decode yolo.py:42-63,140-160
+ *   yv7_nms           non_max_suppression()                   utils/general.py:628-720 incl. the
+ *                     torchvision.ops.nms call at general.py:704
+ *   yv7_end2end       TRT EfficientNMS_TRT plugin contract    models/experimental.py:111-156,
+ *                     utils/add_nms.py:94-138 (fixed-shape num_dets/boxes/scores/classes)
+ */
+#ifndef YV7_H
+#define YV7_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define YV7_ABI_VERSION 1
+
+typedef enum {
+  YV7_OK = 0,
+  YV7_E_ARG = -1,       /* bad argument (null pointer, bad enum) */
+  YV7_E_SHAPE = -2,     /* shape not supported by the plan (e.g. H/W not a multiple of max stride) */
+  YV7_E_WORKSPACE = -3, /* workspace too small */
+  YV7_E_ABI = -4,       /* descriptor abi_version mismatch */
+  YV7_E_DEVICE = -5     /* no gfx950 device / wrong device */
+} yv7_status;
+
+typedef enum { YV7_DT_F32 = 0, YV7_DT_F16 = 1 } yv7_dtype;
+typedef enum { YV7_ACT_NONE = 0, YV7_ACT_SILU = 1, YV7_ACT_LEAKY = 2 } yv7_act;
+
+typedef enum {
+  YV7_OP_INPUT = 0,    /* NCHW image batch -> NHWC tensor; k=2 means fused ReOrg space-to-depth */
+  YV7_OP_CONV = 1,     /* k x k conv, stride s, pad, + fp32 bias + act; NHWC channel slices in/out */
+  YV7_OP_MAXPOOL = 2,  /* max pool k, stride s, pad (implicit -inf padding) */
+  YV7_OP_UPSAMPLE = 3, /* nearest-neighbour x2 */
+  YV7_OP_COPY = 4,     /* channel-slice copy (concat input that could not be written in place) */
+  YV7_OP_DETECT = 5    /* 1x1 conv + bias + sigmoid + grid/anchor decode -> z rows, raw logits */
+} yv7_op_kind;
+
+/* One NHWC activation tensor of the plan: [B, H >> shift, W >> shift, channels]. Tensor 0 is the
+ * packed network input written by YV7_OP_INPUT. */
+typedef struct {
+  int32_t channels; /* channel count == row pitch in elements (multiple of 8) */
+  int32_t shift;    /* log2 spatial downsampling relative to the network input */
+} yv7_tensor_desc;
+
+typedef struct {
+  int32_t kind;                /* yv7_op_kind */
+  int32_t src, src_coff, cin;  /* input tensor, channel offset, channels read */
+  int32_t dst, dst_coff, cout; /* output tensor, channel offset, channels written */
+  int32_t k, s, pad, act;      /* window / stride / padding / yv7_act */
+  int32_t level;               /* DETECT: head level */
+  int64_t w_off;               /* CONV/DETECT: byte offset of weights [cout_pad][k][k][cin], K padded to 32 */
+  int64_t b_off;               /* CONV/DETECT: byte offset of fp32 bias [cout_pad] */
+} yv7_op_desc;
+
+typedef struct {
+  int32_t abi_version;   /* YV7_ABI_VERSION */
+  int32_t dtype;         /* yv7_dtype of activations and packed weights */
+  int32_t n_tensors;
+  const yv7_tensor_desc* tensors;
+  int32_t n_ops;
+  const yv7_op_desc* ops;
+  int32_t nl, na, no;    /* detection levels, anchors per level, outputs per anchor (nc + 5) */
+  const float* stride;   /* [nl] */
+  const float* anchor_grid; /* [nl][na][2] anchor sizes in pixels (Detect.anchor_grid) */
+  int32_t max_shift;     /* input H and W must be multiples of 1 << max_shift */
+} yv7_net_desc;
+
+typedef struct yv7_plan yv7_plan;
+
+int32_t yv7_abi_version(void);
+const char* yv7_last_error(void);
+
+/* weights: host or device pointer to the packed blob (copied into plan-owned device memory). */
+int yv7_plan_create(const yv7_net_desc* desc, const void* weights, size_t nbytes, int device,
+                    yv7_plan** out);
+void yv7_plan_destroy(yv7_plan* plan);
+
+/* Bytes of caller-provided workspace yv7_forward needs for a [B,3,H,W] batch. */
+size_t yv7_workspace_bytes(const yv7_plan* plan, int B, int H, int W);
+/* Rows of z per image: sum over levels of na * (H >> s_l) * (W >> s_l). */
+int64_t yv7_num_rows(const yv7_plan* plan, int H, int W);
+
+/* x: [B,3,H,W] (x_dtype f32 or f16, values in [0,1]) on the plan's device.
+ * z_out: [B, N, no] fp32 decoded boxes (Detect z).  raw_out (nullable): per level l the raw head
+ * logits [B, na, ny_l, nx_l, no] fp32, levels concatenated.  Asynchronous on `stream`. */
+int yv7_forward(yv7_plan* plan, const void* x, int x_dtype, int B, int H, int W, float* z_out,
+                float* raw_out, void* workspace, size_t ws_bytes, void* stream);
+
+/* Byte offset of activation tensor `tensor_id` inside the forward workspace and its NHWC dims
+ * [B, H', W', channels] — lets a caller read any intermediate layer for per-layer parity checks. */
+int yv7_tensor_info(const yv7_plan* plan, int tensor_id, int B, int H, int W, int64_t* offset,
+                    int64_t* dims4);
+
+/* Batched NMS over z [B,N,no] fp32, the semantics of utils/general.py:628-720.
+ * det: [B,max_det,6] (x1,y1,x2,y2,conf,cls), src_row: [B,max_det] int64 anchor row of each kept
+ * box, count: [B] int32.  classes: nullable [ncls] int32 class filter. */
+size_t yv7_nms_workspace_bytes(int B, int N, int no, int multi_label, int max_nms);
+int yv7_nms(const float* z, int B, int N, int no, float conf_thres, float iou_thres, int multi_label,
+            int agnostic, const int32_t* classes, int ncls, int max_det, int max_nms, float* det,
+            int64_t* src_row, int32_t* count, void* workspace, size_t ws_bytes, void* stream);
+
+/* EfficientNMS_TRT-shaped output (End2End, experimental.py:226-241): num_dets int32 [B,1],
+ * det_boxes [B,topk,4], det_scores [B,topk], det_classes int32 [B,topk]; zero-padded. */
+size_t yv7_end2end_workspace_bytes(int B, int N, int no, int topk);
+int yv7_end2end(const float* z, int B, int N, int no, float conf_thres, float iou_thres, int topk,
+                int32_t* num_dets, float* det_boxes, float* det_scores, int32_t* det_classes,
+                void* workspace, size_t ws_bytes, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* YV7_H */

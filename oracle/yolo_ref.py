@@ -1,0 +1,325 @@
+"""TEST INFRASTRUCTURE ONLY — CPU restatement of the reference YOLOv7 inference path (fp32, NCHW).
+
+See oracle/__init__.py for who may import this and for the parity-pinning status.
+
+This file restates, from the reference sources read as text (never imported or executed):
+  * parse_model                 models/yolo.py:736-813 (+ make_divisible utils/general.py:177-179,
+                                autopad models/common.py:23-27)
+  * stride / anchor setup       models/yolo.py:542-548, utils/autoanchor.py:12-20
+  * BN folding                  utils/torch_utils.py:181-201 (Conv), models/common.py:561-643 (RepConv)
+  * IDetect implicit folding    models/yolo.py:178-190 (also IAuxDetect 411-423)
+  * forward_once                models/yolo.py:601-631
+  * layer forwards              Conv.fuseforward common.py:110-111, RepConv deploy common.py:498-500,
+                                SPPCSPC common.py:276-280, MP 30-36, SP 39-45, ReOrg 48-53, Concat 56-62
+  * Detect decode               models/yolo.py:42-63 (== IDetect.fuseforward 140-160)
+It is written as plain functions over a layer table and a reference-keyed state_dict, so the
+same synthetic weights can be fed to the product (models.yolo.Model.load_state_dict) and here.
+"""
+from __future__ import annotations
+
+import math
+import re
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn.functional as F
+
+BN_EPS = 1e-3  # initialize_weights sets eps=1e-3 on every BatchNorm2d (utils/torch_utils.py:144-153)
+
+
+def make_divisible(x, divisor):  # utils/general.py:177-179
+    return math.ceil(x / divisor) * divisor
+
+
+def autopad(k, p=None):  # models/common.py:23-27
+    return k // 2 if p is None else p
+
+
+_LEAKY = re.compile(r'nn\.LeakyReLU\(\s*([-+0-9.eE]+)\s*\)')
+
+
+def _eval_arg(a, nc, anchors):
+    """Stand-in for the `eval(a)` of string args in parse_model (models/yolo.py:745-749)."""
+    if not isinstance(a, str):
+        return a
+    if a == 'None':
+        return None
+    if a == 'nc':
+        return nc
+    if a == 'anchors':
+        return anchors
+    if a in ('True', 'False'):
+        return a == 'True'
+    m = _LEAKY.fullmatch(a)
+    if m:
+        return ('leaky', float(m.group(1)))
+    if a == 'nn.SiLU()':
+        return ('silu',)
+    if a == 'nn.Identity()':
+        return ('none',)
+    return a  # e.g. 'nearest' stays a string, exactly as the bare eval failure leaves it
+
+
+@dataclass
+class Layer:
+    i: int
+    f: object
+    type: str
+    c1: object
+    c2: int
+    p: dict = field(default_factory=dict)
+
+
+@dataclass
+class Net:
+    layers: list
+    save: list
+    nc: int
+    na: int
+    no: int
+    nl: int
+    anchors: list
+    stride: list = None
+    anchor_grid: torch.Tensor = None  # [nl, na, 2] pixels
+
+
+def _act_of(a):
+    if a is True or a is None:
+        return ('silu',)
+    if a is False:
+        return ('none',)
+    return a
+
+
+def parse(d: dict, ch_in: int = 3) -> Net:
+    """Restates parse_model (models/yolo.py:736-813) for the module subset of the yolov7 family."""
+    anchors, nc, gd, gw = d['anchors'], d['nc'], d['depth_multiple'], d['width_multiple']
+    na = (len(anchors[0]) // 2) if isinstance(anchors, list) else anchors
+    no = na * (nc + 5)
+    layers, save, ch = [], [], [ch_in]
+    c2 = ch_in
+    for i, (f, n, m, args) in enumerate(d['backbone'] + d['head']):
+        args = [_eval_arg(a, nc, anchors) for a in args]
+        if n > 1:
+            n = max(round(n * gd), 1)
+        if n != 1:
+            raise NotImplementedError('repeated modules are not used by the yolov7 family cfgs')
+        p = {}
+        if m in ('Conv', 'RepConv', 'SPPCSPC'):
+            c1, c2 = ch[f], args[0]
+            if c2 != no:
+                c2 = make_divisible(c2 * gw, 8)
+            if m == 'SPPCSPC':
+                p['c_'] = int(2 * c2 * 0.5)  # common.py:266 (e=0.5)
+                p['pools'] = (5, 9, 13)
+            else:
+                k = args[1] if len(args) > 1 else (3 if m == 'RepConv' else 1)
+                s = args[2] if len(args) > 2 else 1
+                pad = autopad(k, args[3] if len(args) > 3 else None)
+                g = args[4] if len(args) > 4 else 1
+                if g != 1:
+                    raise NotImplementedError('grouped conv')
+                act = _act_of(args[5] if len(args) > 5 else True)
+                p.update(k=k, s=s, pad=pad, act=act)
+        elif m == 'Concat':
+            c1, c2 = [ch[x] for x in f], sum(ch[x] for x in f)
+        elif m in ('Detect', 'IDetect', 'IAuxDetect'):
+            c1, c2 = [ch[x] for x in f], 0
+        elif m == 'ReOrg':
+            c1, c2 = ch[f], ch[f] * 4
+        elif m == 'MP':
+            c1 = c2 = ch[f]
+            p['k'] = args[0] if args else 2
+        elif m == 'SP':
+            c1 = c2 = ch[f]
+            p['k'] = args[0] if args else 3
+            p['s'] = args[1] if len(args) > 1 else 1
+        elif m == 'nn.Upsample':
+            c1 = c2 = ch[f]
+            p['scale'] = args[1]
+            p['mode'] = args[2]
+        else:
+            raise NotImplementedError(f'module {m} is outside the yolov7-family hot path')
+        layers.append(Layer(i, f, m, c1, c2, p))
+        save.extend(x % i for x in ([f] if isinstance(f, int) else f) if x != -1)
+        if i == 0:
+            ch = []
+        ch.append(c2)
+    net = Net(layers, sorted(save), nc, na, nc + 5, len(anchors), anchors)
+    _setup_strides(net)
+    return net
+
+
+def _levels(net: Net):
+    """Spatial downsampling factor (log2) of every layer output (what the 256x256 probe forward measures)."""
+    lv = []
+    for L in net.layers:
+        src = L.f if isinstance(L.f, int) else L.f[0]
+        prev = 0 if L.i == 0 else (lv[-1] if src == -1 else lv[src])
+        t = L.type
+        if t in ('Conv', 'RepConv'):
+            v = prev + (1 if L.p['s'] == 2 else 0)
+        elif t in ('MP', 'ReOrg'):
+            v = prev + 1
+        elif t == 'nn.Upsample':
+            v = prev - 1
+        else:
+            v = prev
+        lv.append(v)
+    return lv
+
+
+def _setup_strides(net: Net):
+    """models/yolo.py:542-548: stride = 256 / H_out of a 256x256 probe; check_anchor_order (autoanchor.py:12-20)."""
+    lv = _levels(net)
+    det = net.layers[-1]
+    srcs = det.f[:net.nl]
+    net.stride = [float(2 ** lv[j]) for j in srcs]
+    ag = torch.tensor(net.anchors, dtype=torch.float32).view(net.nl, -1, 2)
+    a = ag.prod(-1).view(-1)
+    da = a[-1] - a[0]
+    ds = net.stride[-1] - net.stride[0]
+    sign_ds = 0.0 if ds == 0 else math.copysign(1.0, ds)
+    if float(da.sign()) != sign_ds:  # 'Reversing anchor order'
+        ag = ag.flip(0)
+    net.anchor_grid = ag.clone()
+
+
+# ---------------------------------------------------------------- folding (attempt_load -> fuse)
+
+def fuse_conv_and_bn(w, gamma, beta, mean, var, eps=BN_EPS):
+    """utils/torch_utils.py:181-201 (conv without bias)."""
+    co = w.shape[0]
+    w_bn = torch.diag(gamma.div(torch.sqrt(eps + var)))
+    wf = torch.mm(w_bn, w.clone().view(co, -1)).view(w.shape)
+    b_conv = torch.zeros(co, dtype=w.dtype)
+    b_bn = beta - gamma.mul(mean).div(torch.sqrt(var + eps))
+    bf = torch.mm(w_bn, b_conv.reshape(-1, 1)).reshape(-1) + b_bn
+    return wf, bf
+
+
+def _repconv_branch(w, gamma, beta, mean, var, eps=BN_EPS):
+    """RepConv.fuse_conv_bn (models/common.py:561-582)."""
+    std = (var + eps).sqrt()
+    b = beta - mean * gamma / std
+    t = (gamma / std).reshape(-1, 1, 1, 1)
+    return w * t, b
+
+
+def _bn(sd, prefix):
+    return (sd[prefix + '.weight'].float(), sd[prefix + '.bias'].float(),
+            sd[prefix + '.running_mean'].float(), sd[prefix + '.running_var'].float())
+
+
+def fuse(net: Net, sd: dict) -> dict:
+    """Fold a reference-keyed state_dict into per-conv (W, b) fp32 tensors (Model.fuse, yolo.py:693-710).
+
+    Keys follow the reference module tree: model.{i}.conv.weight + model.{i}.bn.*,
+    model.{i}.rbr_dense.{0,1}.* / rbr_1x1.{0,1}.*, model.{i}.cv{1..7}.*, model.{i}.m.{j}.*, ia/im.
+    """
+    sd = {k: v.float() if v.is_floating_point() else v for k, v in sd.items()}
+    out = {}
+    for L in net.layers:
+        pre = f'model.{L.i}'
+        if L.type == 'Conv':
+            out[L.i] = fuse_conv_and_bn(sd[pre + '.conv.weight'], *_bn(sd, pre + '.bn'))
+        elif L.type == 'RepConv':
+            w3, b3 = _repconv_branch(sd[pre + '.rbr_dense.0.weight'], *_bn(sd, pre + '.rbr_dense.1'))
+            w1, b1 = _repconv_branch(sd[pre + '.rbr_1x1.0.weight'], *_bn(sd, pre + '.rbr_1x1.1'))
+            # identity branch is None because c1 != c2 in every yolov7 RepConv (common.py:486)
+            if L.c1 == L.c2 and L.p['s'] == 1:
+                raise NotImplementedError('RepConv identity branch')
+            w1p = F.pad(w1, [1, 1, 1, 1])
+            out[L.i] = (w3 + w1p + torch.zeros_like(w1p), b3 + b1 + torch.zeros_like(b1))
+        elif L.type == 'SPPCSPC':
+            out[L.i] = {j: fuse_conv_and_bn(sd[f'{pre}.cv{j}.conv.weight'], *_bn(sd, f'{pre}.cv{j}.bn'))
+                        for j in range(1, 8)}
+        elif L.type in ('Detect', 'IDetect', 'IAuxDetect'):
+            heads = []
+            for j in range(net.nl):
+                w = sd[f'{pre}.m.{j}.weight'].clone()
+                b = sd[f'{pre}.m.{j}.bias'].clone()
+                if L.type != 'Detect':  # IDetect.fuse (yolo.py:178-190)
+                    c1, c2 = w.shape[:2]
+                    ia = sd[f'{pre}.ia.{j}.implicit']
+                    b += torch.matmul(w.reshape(c1, c2), ia.reshape(ia.shape[1], ia.shape[0])).squeeze(1)
+                    im = sd[f'{pre}.im.{j}.implicit']
+                    b *= im.reshape(im.shape[1])
+                    w *= im.transpose(0, 1)
+                heads.append((w, b))
+            out[L.i] = heads
+    return out
+
+
+# ---------------------------------------------------------------- forward (NCHW fp32)
+
+def _act(x, act):
+    if act[0] == 'silu':
+        return F.silu(x)
+    if act[0] == 'leaky':
+        return F.leaky_relu(x, act[1])
+    return x
+
+
+def _conv(x, wb, k, s, pad, act):
+    return _act(F.conv2d(x, wb[0], wb[1], s, pad), act)
+
+
+def _make_grid(nx, ny):  # models/yolo.py:79-82
+    yv, xv = torch.meshgrid([torch.arange(ny), torch.arange(nx)], indexing='ij')
+    return torch.stack((xv, yv), 2).view((1, 1, ny, nx, 2)).float()
+
+
+def detect_decode(net: Net, raw: list):
+    """Detect.forward inference branch (models/yolo.py:46-63) given the per-level conv outputs."""
+    z, xs = [], []
+    for i, v in enumerate(raw):
+        bs, _, ny, nx = v.shape
+        v = v.view(bs, net.na, net.no, ny, nx).permute(0, 1, 3, 4, 2).contiguous()
+        xs.append(v)
+        grid = _make_grid(nx, ny)
+        ag = net.anchor_grid[i].view(1, net.na, 1, 1, 2)
+        y = v.sigmoid()
+        y[..., 0:2] = (y[..., 0:2] * 2. - 0.5 + grid) * net.stride[i]
+        y[..., 2:4] = (y[..., 2:4] * 2) ** 2 * ag
+        z.append(y.view(bs, -1, net.no))
+    return torch.cat(z, 1), xs
+
+
+def forward(net: Net, fused: dict, x: torch.Tensor, return_all=False):
+    """forward_once (models/yolo.py:601-631) on the fused (deploy) network; returns (z, xs)."""
+    y = []
+    outs = {}
+    for L in net.layers:
+        if L.f != -1:
+            x = y[L.f] if isinstance(L.f, int) else [x if j == -1 else y[j] for j in L.f]
+        t = L.type
+        if t in ('Conv', 'RepConv'):
+            x = _conv(x, fused[L.i], L.p['k'], L.p['s'], L.p['pad'], L.p['act'])
+        elif t == 'SPPCSPC':
+            cv = fused[L.i]
+            silu = ('silu',)
+            x1 = _conv(_conv(_conv(x, cv[1], 1, 1, 0, silu), cv[3], 3, 1, 1, silu), cv[4], 1, 1, 0, silu)
+            cat = torch.cat([x1] + [F.max_pool2d(x1, k, 1, k // 2) for k in L.p['pools']], 1)
+            y1 = _conv(_conv(cat, cv[5], 1, 1, 0, silu), cv[6], 3, 1, 1, silu)
+            y2 = _conv(x, cv[2], 1, 1, 0, silu)
+            x = _conv(torch.cat((y1, y2), dim=1), cv[7], 1, 1, 0, silu)
+        elif t == 'MP':
+            x = F.max_pool2d(x, L.p['k'], L.p['k'])
+        elif t == 'SP':
+            x = F.max_pool2d(x, L.p['k'], L.p['s'], L.p['k'] // 2)
+        elif t == 'Concat':
+            x = torch.cat(x, 1)
+        elif t == 'nn.Upsample':
+            x = F.interpolate(x, scale_factor=float(L.p['scale']), mode=L.p['mode'])
+        elif t == 'ReOrg':
+            x = torch.cat([x[..., ::2, ::2], x[..., 1::2, ::2], x[..., ::2, 1::2], x[..., 1::2, 1::2]], 1)
+        elif t in ('Detect', 'IDetect', 'IAuxDetect'):
+            raw = [F.conv2d(x[j], fused[L.i][j][0], fused[L.i][j][1]) for j in range(net.nl)]
+            x = detect_decode(net, raw)
+        else:
+            raise NotImplementedError(t)
+        if return_all:
+            outs[L.i] = x
+        y.append(x if L.i in net.save else None)
+    return (x, outs) if return_all else x

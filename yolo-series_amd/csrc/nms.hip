@@ -1,0 +1,490 @@
+// Batched non_max_suppression on gfx950 — the semantics of utils/general.py:628-720 with the
+// torchvision.ops.nms call (general.py:704) restated as a blocked greedy scan.
+//
+// Pipeline (all images of the batch in one launch per stage, no host sync):
+//   1 nms_rows     one wave per anchor row: obj > conf (:637,:653), conf = cls*obj (:669-673),
+//                  single-label first-max argmax (:683-684) or multi-label class mask (:680-681),
+//                  optional class filter (:687-688) -> per-row candidate count (+best conf/cls)
+//   2 nms_scan     per-image exclusive scan of the counts -> stable row-order offsets
+//   3 nms_write    candidate records {xyxy (:676, xywh2xyxy :275-282), conf, cls, row} in the
+//                  reference's candidate order (row-major, classes ascending)
+//   4 nms_sort     per-image sort by (score desc, candidate index asc) == torchvision's stable
+//                  descending sort; bitonic in LDS up to 16384 candidates, in global memory above;
+//                  the first max_nms (:698-699) go on
+//   5 nms_greedy   blocked greedy NMS on class-offset boxes (:702-703, max_wh 4096): a wave resolves
+//                  64 sorted candidates at a time, the workgroup then strikes later candidates that
+//                  a box kept in that block overlaps (IoU > thr); stops at max_det kept (:705-706).
+// IoU arithmetic is torchvision's: area=(x2-x1)*(y2-y1), inter=max(0,.)*max(0,.),
+// inter / (area_i + area_j - inter) > thr, all fp32; this file is built with -ffp-contract=off.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace yv7 {
+
+namespace {
+
+constexpr int NT = 256;
+constexpr int SORT_T = 1024;
+constexpr int LDS_SORT_MAX = 16384;
+constexpr int MAX_WH = 4096;
+
+struct Cand {
+  float x1, y1, x2, y2, conf;
+  int cls, row, pad;
+};
+
+struct NmsArgs {
+  const float* z;
+  int B, N, no, nc;
+  float conf, iou;
+  int multi, agnostic, per_class;  // per_class: class-aware IoU on raw boxes (EfficientNMS) instead of offsets
+  const int32_t* classes;
+  int ncls;
+  int max_det, max_nms;
+  size_t cap;   // candidate capacity per image
+  size_t pcap;  // pow2 >= cap: per-image stride of the global sort keys
+  // workspace
+  int* cnt;         // [B][N]
+  int* offs;        // [B][N]
+  float* bconf;     // [B][N] single-label best conf
+  int* bcls;        // [B][N]
+  int* ncand;       // [B]
+  Cand* cand;       // [B][cap]
+  uint64_t* keys;   // [B][pow2(cap)]
+  int* order;       // [B][max_nms]
+  float4* sbox;     // [B][max_nms] offset boxes in sorted order
+  float* sarea;     // [B][max_nms]
+  // outputs
+  float* det;       // [B][max_det][6]
+  int64_t* src_row; // [B][max_det]
+  int32_t* count;   // [B]
+};
+
+__device__ __forceinline__ bool class_ok(const NmsArgs& a, int c) {
+  if (!a.classes) return true;
+  for (int i = 0; i < a.ncls; ++i)
+    if (a.classes[i] == c) return true;
+  return false;
+}
+
+// Stage 1: one wave per row. Lanes hold classes c and c+64.
+__global__ __launch_bounds__(NT) void nms_rows(const NmsArgs a) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * NT + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * NT) >> 6;
+  for (int row = wave; row < a.N; row += nwaves) {
+    const float* zr = a.z + ((size_t)b * a.N + row) * a.no;
+    const float obj = zr[4];
+    int cnt = 0;
+    float best = 0.f;
+    int bc = 0;
+    if (obj > a.conf) {
+      float v0 = -1.f, v1 = -1.f;
+      const int c0 = lane, c1 = lane + 64;
+      if (a.nc == 1) {
+        v0 = (c0 == 0) ? obj : -1.f;  // nc == 1: conf = obj (:669-670)
+      } else {
+        if (c0 < a.nc) v0 = zr[5 + c0] * obj;
+        if (c1 < a.nc) v1 = zr[5 + c1] * obj;
+      }
+      if (a.multi) {
+        const bool p0 = c0 < a.nc && v0 > a.conf && class_ok(a, c0);
+        const bool p1 = c1 < a.nc && v1 > a.conf && class_ok(a, c1);
+        cnt = __popcll(__ballot(p0)) + __popcll(__ballot(p1));
+      } else {
+        // first max over classes: strict > keeps the lower class index on ties
+        float v = v0;
+        int c = c0;
+        if (c1 < a.nc && v1 > v0) { v = v1; c = c1; }
+        if (c0 >= a.nc) { v = -2.f; c = 1 << 30; }
+        for (int off = 32; off > 0; off >>= 1) {
+          const float ov = __shfl_xor(v, off);
+          const int oc = __shfl_xor(c, off);
+          if (ov > v || (ov == v && oc < c)) { v = ov; c = oc; }
+        }
+        best = v;
+        bc = c;
+        cnt = (v > a.conf && class_ok(a, c)) ? 1 : 0;
+      }
+    }
+    if (lane == 0) {
+      const size_t i = (size_t)b * a.N + row;
+      a.cnt[i] = cnt;
+      if (!a.multi) {
+        a.bconf[i] = best;
+        a.bcls[i] = bc;
+      }
+    }
+  }
+}
+
+// Stage 2: per-image exclusive scan (one workgroup of SORT_T threads per image).
+__global__ __launch_bounds__(SORT_T) void nms_scan(const NmsArgs a) {
+  const int b = blockIdx.x;
+  __shared__ int wsum[SORT_T / 64];
+  __shared__ int carry;
+  if (threadIdx.x == 0) carry = 0;
+  __syncthreads();
+  const int* cnt = a.cnt + (size_t)b * a.N;
+  int* offs = a.offs + (size_t)b * a.N;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int base = 0; base < a.N; base += SORT_T) {
+    const int i = base + threadIdx.x;
+    const int v = i < a.N ? cnt[i] : 0;
+    int s = v;  // inclusive wave scan
+    for (int off = 1; off < 64; off <<= 1) {
+      const int t = __shfl_up(s, off);
+      if (lane >= off) s += t;
+    }
+    if (lane == 63) wsum[wv] = s;
+    __syncthreads();
+    int pre = carry;
+    for (int k = 0; k < wv; ++k) pre += wsum[k];
+    if (i < a.N) offs[i] = pre + s - v;
+    __syncthreads();
+    if (threadIdx.x == SORT_T - 1) carry = pre + s;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.ncand[b] = carry;
+}
+
+// Stage 3: write candidate records in reference order.
+__global__ __launch_bounds__(NT) void nms_write(const NmsArgs a) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * NT + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * NT) >> 6;
+  for (int row = wave; row < a.N; row += nwaves) {
+    const size_t ri = (size_t)b * a.N + row;
+    const int cnt = a.cnt[ri];
+    if (cnt == 0) continue;
+    const float* zr = a.z + ri * a.no;
+    const float cx = zr[0], cy = zr[1], w = zr[2], h = zr[3];
+    Cand c;
+    c.x1 = cx - w / 2.0f;  // xywh2xyxy (general.py:275-282)
+    c.y1 = cy - h / 2.0f;
+    c.x2 = cx + w / 2.0f;
+    c.y2 = cy + h / 2.0f;
+    c.row = row;
+    c.pad = 0;
+    Cand* out = a.cand + (size_t)b * a.cap + a.offs[ri];
+    if (!a.multi) {
+      if (lane == 0) {
+        c.conf = a.bconf[ri];
+        c.cls = a.bcls[ri];
+        out[0] = c;
+      }
+    } else {
+      const float obj = zr[4];
+      const int c0 = lane, c1 = lane + 64;
+      float v0 = -1.f, v1 = -1.f;
+      if (a.nc == 1) {
+        v0 = (c0 == 0) ? obj : -1.f;
+      } else {
+        if (c0 < a.nc) v0 = zr[5 + c0] * obj;
+        if (c1 < a.nc) v1 = zr[5 + c1] * obj;
+      }
+      const bool p0 = c0 < a.nc && v0 > a.conf && class_ok(a, c0);
+      const bool p1 = c1 < a.nc && v1 > a.conf && class_ok(a, c1);
+      const uint64_t m0 = __ballot(p0), m1 = __ballot(p1);
+      const uint64_t below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+      if (p0) {
+        Cand d = c;
+        d.conf = v0;
+        d.cls = c0;
+        out[__popcll(m0 & below)] = d;
+      }
+      if (p1) {
+        Cand d = c;
+        d.conf = v1;
+        d.cls = c1;
+        out[__popcll(m0) + __popcll(m1 & below)] = d;
+      }
+    }
+  }
+}
+
+__device__ __forceinline__ uint64_t sort_key(float conf, int idx) {
+  // conf > conf_thres >= 0 here, so the fp32 bit pattern orders like the value.
+  return ((uint64_t)(~__float_as_uint(conf)) << 32) | (uint32_t)idx;
+}
+
+// Stage 4: per-image sort -> order[] of the first min(n, max_nms) candidates.
+__global__ __launch_bounds__(SORT_T) void nms_sort(const NmsArgs a) {
+  const int b = blockIdx.x;
+  const int n = a.ncand[b];
+  const Cand* cand = a.cand + (size_t)b * a.cap;
+  int* order = a.order + (size_t)b * a.max_nms;
+  const int keep = n < a.max_nms ? n : a.max_nms;
+  if (n == 0) return;
+  int P = 1;
+  while (P < n) P <<= 1;
+  extern __shared__ __attribute__((aligned(16))) uint64_t skeys[];
+  const bool in_lds = P <= LDS_SORT_MAX;
+  uint64_t* keys = in_lds ? skeys : a.keys + (size_t)b * a.pcap;
+  for (int i = threadIdx.x; i < P; i += SORT_T) keys[i] = i < n ? sort_key(cand[i].conf, i) : ~0ull;
+  __syncthreads();
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      for (int i = threadIdx.x; i < P; i += SORT_T) {
+        const int ixj = i ^ j;
+        if (ixj > i) {
+          const uint64_t ki = keys[i], kj = keys[ixj];
+          const bool up = (i & k) == 0;
+          if ((ki > kj) == up) {
+            keys[i] = kj;
+            keys[ixj] = ki;
+          }
+        }
+      }
+      __syncthreads();
+    }
+  }
+  for (int i = threadIdx.x; i < keep; i += SORT_T) order[i] = (int)(uint32_t)keys[i];
+}
+
+__device__ __forceinline__ bool iou_gt(const float4 bi, float ai, const float4 bj, float aj, float thr) {
+  // torchvision nms: i is the kept box
+  const float xx1 = fmaxf(bi.x, bj.x), yy1 = fmaxf(bi.y, bj.y);
+  const float xx2 = fminf(bi.z, bj.z), yy2 = fminf(bi.w, bj.w);
+  const float w = fmaxf(0.0f, xx2 - xx1), h = fmaxf(0.0f, yy2 - yy1);
+  const float inter = w * h;
+  return inter / (ai + aj - inter) > thr;
+}
+
+// Stage 5: blocked greedy NMS, one workgroup per image.
+__global__ __launch_bounds__(SORT_T) void nms_greedy(const NmsArgs a) {
+  const int b = blockIdx.x;
+  const int n0 = a.ncand[b];
+  const int n = n0 < a.max_nms ? n0 : a.max_nms;
+  const Cand* cand = a.cand + (size_t)b * a.cap;
+  const int* order = a.order + (size_t)b * a.max_nms;
+  float4* sbox = a.sbox + (size_t)b * a.max_nms;
+  float* sarea = a.sarea + (size_t)b * a.max_nms;
+  extern __shared__ __attribute__((aligned(16))) unsigned char gsm[];
+  uint32_t* removed = reinterpret_cast<uint32_t*>(gsm);            // [max_nms/32 + 2]
+  const int nwords = (n + 31) / 32 + 2;
+  float4* kbox = reinterpret_cast<float4*>(gsm + ((nwords * 4 + 15) / 16) * 16);
+  float* karea = reinterpret_cast<float*>(kbox + 64);
+  int* kcls = reinterpret_cast<int*>(karea + 64);
+  __shared__ int nk_blk, total;
+
+  // gather boxes in sorted order (class-offset unless agnostic / per-class)
+  for (int i = threadIdx.x; i < n; i += SORT_T) {
+    const Cand c = cand[order[i]];
+    const float off = (a.agnostic || a.per_class) ? 0.0f : (float)c.cls * (float)MAX_WH;
+    float4 bx;
+    bx.x = c.x1 + off;
+    bx.y = c.y1 + off;
+    bx.z = c.x2 + off;
+    bx.w = c.y2 + off;
+    sbox[i] = bx;
+    sarea[i] = (bx.z - bx.x) * (bx.w - bx.y);
+  }
+  for (int i = threadIdx.x; i < nwords; i += SORT_T) removed[i] = 0u;
+  if (threadIdx.x == 0) total = 0;
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  for (int base = 0; base < n; base += 64) {
+    if (threadIdx.x < 64) {
+      const int j = base + lane;
+      const bool valid = j < n;
+      float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
+      float aj = 0.f;
+      int cj = -1;
+      if (valid) {
+        bj = sbox[j];
+        aj = sarea[j];
+        if (a.per_class) cj = cand[order[j]].cls;
+      }
+      bool rem = !valid || ((removed[j >> 5] >> (j & 31)) & 1u);
+      uint64_t kept = 0;
+      uint64_t alive = __ballot(!rem);
+      while (alive) {
+        const int i = __ffsll((long long)alive) - 1;
+        kept |= 1ull << i;
+        const float4 bi = make_float4(__shfl(bj.x, i), __shfl(bj.y, i), __shfl(bj.z, i), __shfl(bj.w, i));
+        const float ai = __shfl(aj, i);
+        const int ci = __shfl(cj, i);
+        if (lane > i && !rem && (!a.per_class || ci == cj) && iou_gt(bi, ai, bj, aj, a.iou)) rem = true;
+        alive = (i == 63) ? 0ull : (__ballot(!rem) & ~((2ull << i) - 1ull));
+      }
+      const int nk = __popcll(kept);
+      const bool mine = (kept >> lane) & 1ull;
+      const int rank = __popcll(kept & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+      if (mine) {
+        kbox[rank] = bj;
+        karea[rank] = aj;
+        kcls[rank] = cj;
+        const int di = total + rank;
+        if (di < a.max_det) {
+          const Cand c = cand[order[base + lane]];
+          float* d = a.det + ((size_t)b * a.max_det + di) * 6;
+          d[0] = c.x1;
+          d[1] = c.y1;
+          d[2] = c.x2;
+          d[3] = c.y2;
+          d[4] = c.conf;
+          d[5] = (float)c.cls;
+          a.src_row[(size_t)b * a.max_det + di] = c.row;
+        }
+      }
+      if (lane == 0) nk_blk = nk;
+    }
+    __syncthreads();
+    const int nk = nk_blk;
+    if (threadIdx.x == 0) total += nk;
+    __syncthreads();
+    if (total >= a.max_det) break;
+    // strike later candidates overlapped by a box kept in this block
+    const int w0 = (base + 64) >> 5;
+    const int wend = (n + 31) >> 5;
+    if (nk > 0) {
+      for (int wi = w0 + threadIdx.x; wi < wend; wi += SORT_T) {
+        uint32_t word = removed[wi];
+        for (int bit = 0; bit < 32; ++bit) {
+          const int j = wi * 32 + bit;
+          if (j >= n || ((word >> bit) & 1u)) continue;
+          const float4 bj = sbox[j];
+          const float aj = sarea[j];
+          const int cj = a.per_class ? cand[order[j]].cls : -1;
+          for (int t = 0; t < nk; ++t) {
+            if (a.per_class && kcls[t] != cj) continue;
+            if (iou_gt(kbox[t], karea[t], bj, aj, a.iou)) {
+              word |= 1u << bit;
+              break;
+            }
+          }
+        }
+        removed[wi] = word;
+      }
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) a.count[b] = total < a.max_det ? total : a.max_det;
+}
+
+struct Layout {
+  size_t cnt, offs, bconf, bcls, ncand, cand, keys, order, sbox, sarea, total;
+  size_t cap, pcap;
+};
+
+inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
+
+Layout layout(int B, int N, int nc, int multi, int max_nms) {
+  Layout L;
+  L.cap = (size_t)N * (multi ? (size_t)nc : 1);
+  L.pcap = 1;
+  while (L.pcap < L.cap) L.pcap <<= 1;
+  size_t o = 0;
+  L.cnt = o; o = al(o + sizeof(int) * (size_t)B * N);
+  L.offs = o; o = al(o + sizeof(int) * (size_t)B * N);
+  L.bconf = o; o = al(o + sizeof(float) * (size_t)B * N);
+  L.bcls = o; o = al(o + sizeof(int) * (size_t)B * N);
+  L.ncand = o; o = al(o + sizeof(int) * (size_t)B);
+  L.cand = o; o = al(o + sizeof(Cand) * (size_t)B * L.cap);
+  L.keys = o; o = al(o + (L.pcap > (size_t)LDS_SORT_MAX ? sizeof(uint64_t) * (size_t)B * L.pcap : 0));
+  L.order = o; o = al(o + sizeof(int) * (size_t)B * max_nms);
+  L.sbox = o; o = al(o + sizeof(float4) * (size_t)B * max_nms);
+  L.sarea = o; o = al(o + sizeof(float) * (size_t)B * max_nms);
+  L.total = o;
+  return L;
+}
+
+// End2End / EfficientNMS_TRT output packing (models/experimental.py:144-154, inf_onnx_trt.py:27-36):
+// num_dets int32 [B,1], det_boxes [B,topk,4], det_scores [B,topk], det_classes int32 [B,topk].
+__global__ __launch_bounds__(NT) void end2end_pack(const float* det, const int32_t* count, int B, int max_det, int topk,
+                                                   int32_t* num_dets, float* boxes, float* scores, int32_t* classes) {
+  const int b = blockIdx.x;
+  const int n = count[b] < topk ? count[b] : topk;
+  if (threadIdx.x == 0) num_dets[b] = n;
+  for (int i = threadIdx.x; i < topk; i += NT) {
+    const bool v = i < n;
+    const float* d = det + ((size_t)b * max_det + i) * 6;
+    float* bx = boxes + ((size_t)b * topk + i) * 4;
+    bx[0] = v ? d[0] : 0.f;
+    bx[1] = v ? d[1] : 0.f;
+    bx[2] = v ? d[2] : 0.f;
+    bx[3] = v ? d[3] : 0.f;
+    scores[(size_t)b * topk + i] = v ? d[4] : 0.f;
+    classes[(size_t)b * topk + i] = v ? (int32_t)d[5] : 0;
+  }
+}
+
+}  // namespace
+
+hipError_t launch_end2end_pack(const float* det, const int32_t* count, int B, int max_det, int topk, int32_t* num_dets,
+                               float* boxes, float* scores, int32_t* classes, hipStream_t st) {
+  hipLaunchKernelGGL(end2end_pack, dim3(B), dim3(NT), 0, st, det, count, B, max_det, topk, num_dets, boxes, scores,
+                     classes);
+  return hipGetLastError();
+}
+
+size_t nms_workspace_bytes(int B, int N, int no, int multi, int max_nms) {
+  return layout(B, N, no - 5, multi, max_nms).total;
+}
+
+hipError_t launch_nms(const float* z, int B, int N, int no, float conf, float iou, int multi, int agnostic,
+                      int per_class, const int32_t* classes, int ncls, int max_det, int max_nms, float* det,
+                      int64_t* src_row, int32_t* count, void* ws, hipStream_t st) {
+  const Layout L = layout(B, N, no - 5, multi, max_nms);
+  unsigned char* w = reinterpret_cast<unsigned char*>(ws);
+  NmsArgs a;
+  a.z = z;
+  a.B = B;
+  a.N = N;
+  a.no = no;
+  a.nc = no - 5;
+  a.conf = conf;
+  a.iou = iou;
+  a.multi = multi && a.nc > 1;  // multi_label &= nc > 1 (general.py:646)
+  a.agnostic = agnostic;
+  a.per_class = per_class;
+  a.classes = classes;
+  a.ncls = ncls;
+  a.max_det = max_det;
+  a.max_nms = max_nms;
+  a.cap = L.cap;
+  a.pcap = L.pcap;
+  a.cnt = (int*)(w + L.cnt);
+  a.offs = (int*)(w + L.offs);
+  a.bconf = (float*)(w + L.bconf);
+  a.bcls = (int*)(w + L.bcls);
+  a.ncand = (int*)(w + L.ncand);
+  a.cand = (Cand*)(w + L.cand);
+  a.keys = (uint64_t*)(w + L.keys);
+  a.order = (int*)(w + L.order);
+  a.sbox = (float4*)(w + L.sbox);
+  a.sarea = (float*)(w + L.sarea);
+  a.det = det;
+  a.src_row = src_row;
+  a.count = count;
+  hipError_t e;
+  if ((e = hipMemsetAsync(det, 0, sizeof(float) * 6 * (size_t)B * max_det, st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(src_row, 0xff, sizeof(int64_t) * (size_t)B * max_det, st)) != hipSuccess) return e;
+  int gx = (N + 4 * 8 - 1) / (4 * 8);  // 4 waves per block, ~8 rows per wave
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(nms_rows, dim3(gx, B), dim3(NT), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(nms_scan, dim3(B), dim3(SORT_T), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  hipLaunchKernelGGL(nms_write, dim3(gx, B), dim3(NT), 0, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const size_t sort_lds = sizeof(uint64_t) * LDS_SORT_MAX;
+  static bool attr_set = false;
+  if (!attr_set) {
+    if ((e = hipFuncSetAttribute((const void*)nms_sort, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sort_lds)) !=
+        hipSuccess)
+      return e;
+    attr_set = true;
+  }
+  hipLaunchKernelGGL(nms_sort, dim3(B), dim3(SORT_T), sort_lds, st, a);
+  if ((e = hipGetLastError()) != hipSuccess) return e;
+  const size_t g_lds = (((size_t)(max_nms + 31) / 32 + 2) * 4 + 15) / 16 * 16 + 64 * (16 + 4 + 4);
+  hipLaunchKernelGGL(nms_greedy, dim3(B), dim3(SORT_T), g_lds, st, a);
+  return hipGetLastError();
+}
+
+}  // namespace yv7

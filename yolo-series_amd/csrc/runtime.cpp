@@ -1,0 +1,384 @@
+// libyv7 runtime: the C ABI of include/yv7.h — plan creation (packed weights to HBM), workspace
+// layout, the per-batch launch sequence of the fused network, NMS and the End2End output mode.
+//
+// A plan is the deploy-form network (attempt_load -> Model.fuse, models/experimental.py:247-270)
+// as a flat list of ops over NHWC tensors.  yv7_forward walks that list once per batch, launching
+// one kernel per op on the caller's stream (forward_once's per-layer loop, models/yolo.py:603-627,
+// without the Python dispatch); no allocation, no host sync, so callers can capture it in a graph.
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/yv7.h"
+#include "yv7_kernels.h"
+
+namespace yv7 {
+size_t nms_workspace_bytes(int B, int N, int no, int multi, int max_nms);
+hipError_t launch_nms(const float* z, int B, int N, int no, float conf, float iou, int multi, int agnostic,
+                      int per_class, const int32_t* classes, int ncls, int max_det, int max_nms, float* det,
+                      int64_t* src_row, int32_t* count, void* ws, hipStream_t st);
+hipError_t launch_end2end_pack(const float* det, const int32_t* count, int B, int max_det, int topk,
+                               int32_t* num_dets, float* boxes, float* scores, int32_t* classes, hipStream_t st);
+}  // namespace yv7
+
+struct yv7_plan {
+  int device = 0;
+  int dtype = 0;
+  std::vector<yv7_tensor_desc> tensors;
+  std::vector<yv7_op_desc> ops;
+  int nl = 0, na = 0, no = 0, max_shift = 0;
+  std::vector<float> stride, anchor_grid;
+  void* weights = nullptr;
+  size_t wbytes = 0;
+};
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+  g_err = msg;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* where) {
+  g_err = std::string(where) + ": " + hipGetErrorString(e);
+  return (int)e;
+}
+
+size_t elem_size(int dtype) { return dtype == YV7_DT_F16 ? 2 : 4; }
+size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
+
+// Byte offset of every tensor inside the workspace for a [B,3,H,W] batch.
+std::vector<size_t> tensor_offsets(const yv7_plan* p, int B, int H, int W, size_t* total) {
+  std::vector<size_t> off(p->tensors.size());
+  size_t o = 0;
+  for (size_t i = 0; i < p->tensors.size(); ++i) {
+    const auto& t = p->tensors[i];
+    off[i] = o;
+    o = align256(o + (size_t)B * (H >> t.shift) * (W >> t.shift) * t.channels * elem_size(p->dtype));
+  }
+  *total = o;
+  return off;
+}
+
+int check_hw(const yv7_plan* p, int B, int H, int W) {
+  const int m = (1 << p->max_shift) - 1;
+  if (B <= 0 || H <= 0 || W <= 0 || (H & m) || (W & m))
+    return fail(YV7_E_SHAPE, "input H and W must be positive multiples of " + std::to_string(1 << p->max_shift) +
+                                 " (got B=" + std::to_string(B) + " H=" + std::to_string(H) + " W=" +
+                                 std::to_string(W) + ")");
+  return 0;
+}
+
+int kpad_of(const yv7_op_desc& o) { return (o.k * o.k * o.cin + 31) / 32 * 32; }
+
+}  // namespace
+
+extern "C" {
+
+int32_t yv7_abi_version(void) { return YV7_ABI_VERSION; }
+
+const char* yv7_last_error(void) { return g_err.c_str(); }
+
+int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, int device, yv7_plan** out) {
+  if (!d || !out || (!weights && nbytes)) return fail(YV7_E_ARG, "yv7_plan_create: null argument");
+  *out = nullptr;
+  if (d->abi_version != YV7_ABI_VERSION) return fail(YV7_E_ABI, "yv7_plan_create: abi_version mismatch");
+  if (d->dtype != YV7_DT_F32 && d->dtype != YV7_DT_F16) return fail(YV7_E_ARG, "yv7_plan_create: bad dtype");
+  if (d->n_tensors <= 0 || d->n_ops <= 0 || !d->tensors || !d->ops)
+    return fail(YV7_E_ARG, "yv7_plan_create: empty network");
+  if (d->nl <= 0 || d->nl > 8 || d->na <= 0 || d->na > 4 || d->no < 6 || d->no - 5 > 128)
+    return fail(YV7_E_ARG, "yv7_plan_create: unsupported head geometry (nl<=8, na<=4, nc<=128)");
+  const int vec = d->dtype == YV7_DT_F16 ? 8 : 4;
+  for (int i = 0; i < d->n_tensors; ++i)
+    if (d->tensors[i].channels <= 0 || d->tensors[i].channels % vec || d->tensors[i].shift < 0 ||
+        d->tensors[i].shift > d->max_shift)
+      return fail(YV7_E_ARG, "yv7_plan_create: tensor " + std::to_string(i) + " has bad channels/shift");
+  for (int i = 0; i < d->n_ops; ++i) {
+    const auto& o = d->ops[i];
+    const bool src_ok = o.kind == YV7_OP_INPUT || (o.src >= 0 && o.src < d->n_tensors);
+    const bool dst_ok = o.kind == YV7_OP_DETECT || (o.dst >= 0 && o.dst < d->n_tensors);
+    if (!src_ok || !dst_ok) return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " bad tensor id");
+    if (o.kind == YV7_OP_CONV || o.kind == YV7_OP_DETECT) {
+      if (o.cin % vec || (o.kind == YV7_OP_CONV && o.cout % vec))
+        return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " channels not a multiple of the vector");
+      const size_t wb = (size_t)((o.cout + 31) / 32 * 32) * kpad_of(o) * elem_size(d->dtype);
+      if (o.w_off < 0 || o.b_off < 0 || (size_t)o.w_off + wb > nbytes ||
+          (size_t)o.b_off + sizeof(float) * o.cout > nbytes)
+        return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " weight range outside blob");
+      if (o.kind == YV7_OP_DETECT && (o.level < 0 || o.level >= d->nl || o.cout != d->na * d->no || o.k != 1))
+        return fail(YV7_E_ARG, "yv7_plan_create: bad detect op");
+    }
+    if (o.kind != YV7_OP_INPUT && o.kind != YV7_OP_DETECT) {
+      const int src_c = d->tensors[o.src].channels, dst_c = d->tensors[o.dst].channels;
+      const int cin = o.kind == YV7_OP_CONV ? o.cin : o.cout;
+      if (o.src_coff < 0 || o.src_coff + cin > src_c || o.dst_coff < 0 || o.dst_coff + o.cout > dst_c ||
+          o.src_coff % vec || o.dst_coff % vec)
+        return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " channel slice out of range");
+    }
+  }
+  hipError_t e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  hipDeviceProp_t prop;
+  if ((e = hipGetDeviceProperties(&prop, device)) != hipSuccess) return hip_fail(e, "hipGetDeviceProperties");
+  if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+    return fail(YV7_E_DEVICE, std::string("libyv7 is built for gfx950; device is ") + prop.gcnArchName);
+
+  yv7_plan* p = new yv7_plan();
+  p->device = device;
+  p->dtype = d->dtype;
+  p->tensors.assign(d->tensors, d->tensors + d->n_tensors);
+  p->ops.assign(d->ops, d->ops + d->n_ops);
+  p->nl = d->nl;
+  p->na = d->na;
+  p->no = d->no;
+  p->max_shift = d->max_shift;
+  p->stride.assign(d->stride, d->stride + d->nl);
+  p->anchor_grid.assign(d->anchor_grid, d->anchor_grid + d->nl * d->na * 2);
+  p->wbytes = nbytes;
+  if (nbytes) {
+    if ((e = hipMalloc(&p->weights, nbytes)) != hipSuccess) {
+      delete p;
+      return hip_fail(e, "hipMalloc(weights)");
+    }
+    if ((e = hipMemcpy(p->weights, weights, nbytes, hipMemcpyDefault)) != hipSuccess) {
+      (void)hipFree(p->weights);
+      delete p;
+      return hip_fail(e, "hipMemcpy(weights)");
+    }
+  }
+  *out = p;
+  return 0;
+}
+
+void yv7_plan_destroy(yv7_plan* p) {
+  if (!p) return;
+  if (p->weights) (void)hipFree(p->weights);
+  delete p;
+}
+
+size_t yv7_workspace_bytes(const yv7_plan* p, int B, int H, int W) {
+  if (!p || check_hw(p, B, H, W)) return 0;
+  size_t total = 0;
+  tensor_offsets(p, B, H, W, &total);
+  return total;
+}
+
+int64_t yv7_num_rows(const yv7_plan* p, int H, int W) {
+  if (!p) return -1;
+  int64_t n = 0;
+  for (const auto& o : p->ops)
+    if (o.kind == YV7_OP_DETECT) {
+      const int s = p->tensors[o.src].shift;
+      n += (int64_t)p->na * (H >> s) * (W >> s);
+    }
+  return n;
+}
+
+int yv7_tensor_info(const yv7_plan* p, int id, int B, int H, int W, int64_t* offset, int64_t* dims4) {
+  if (!p || id < 0 || id >= (int)p->tensors.size() || !offset || !dims4) return fail(YV7_E_ARG, "yv7_tensor_info");
+  if (int rc = check_hw(p, B, H, W)) return rc;
+  size_t total = 0;
+  auto off = tensor_offsets(p, B, H, W, &total);
+  *offset = (int64_t)off[id];
+  const auto& t = p->tensors[id];
+  dims4[0] = B;
+  dims4[1] = H >> t.shift;
+  dims4[2] = W >> t.shift;
+  dims4[3] = t.channels;
+  return 0;
+}
+
+int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, float* z, float* raw, void* ws,
+                size_t ws_bytes, void* stream) {
+  if (!p || !x || !z || !ws) return fail(YV7_E_ARG, "yv7_forward: null argument");
+  if (x_dtype != YV7_DT_F32 && x_dtype != YV7_DT_F16) return fail(YV7_E_ARG, "yv7_forward: bad x_dtype");
+  if (int rc = check_hw(p, B, H, W)) return rc;
+  size_t total = 0;
+  const auto off = tensor_offsets(p, B, H, W, &total);
+  if (ws_bytes < total) return fail(YV7_E_WORKSPACE, "yv7_forward: workspace too small (need " +
+                                                         std::to_string(total) + " bytes)");
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  unsigned char* wsb = reinterpret_cast<unsigned char*>(ws);
+  const unsigned char* wb = reinterpret_cast<const unsigned char*>(p->weights);
+  const size_t es = elem_size(p->dtype);
+  const int nrows = (int)yv7_num_rows(p, H, W);
+  // raw-logit and z row offsets of each level
+  std::vector<int> row_off(p->nl, 0);
+  std::vector<size_t> raw_off(p->nl, 0);
+  {
+    std::vector<int> lvl_rows(p->nl, 0);
+    for (const auto& o : p->ops)
+      if (o.kind == YV7_OP_DETECT) {
+        const int s = p->tensors[o.src].shift;
+        lvl_rows[o.level] = p->na * (H >> s) * (W >> s);
+      }
+    int acc = 0;
+    size_t racc = 0;
+    for (int l = 0; l < p->nl; ++l) {
+      row_off[l] = acc;
+      raw_off[l] = racc;
+      acc += lvl_rows[l];
+      racc += (size_t)B * lvl_rows[l] * p->no;
+    }
+  }
+  hipError_t e = hipSuccess;
+  for (size_t i = 0; i < p->ops.size(); ++i) {
+    const auto& o = p->ops[i];
+    switch (o.kind) {
+      case YV7_OP_INPUT: {
+        const auto& t = p->tensors[o.dst];
+        e = yv7::launch_input(p->dtype, x, x_dtype, wsb + off[o.dst], B, H, W, t.channels, o.k == 2, st);
+        break;
+      }
+      case YV7_OP_CONV:
+      case YV7_OP_DETECT: {
+        const auto& ti = p->tensors[o.src];
+        yv7::ConvParams c;
+        std::memset(&c, 0, sizeof(c));
+        c.x = wsb + off[o.src];
+        c.B = B;
+        c.H = H >> ti.shift;
+        c.W = W >> ti.shift;
+        c.xc = ti.channels;
+        c.xoff = o.src_coff;
+        c.cin = o.cin;
+        c.Ho = (c.H + 2 * o.pad - o.k) / o.s + 1;
+        c.Wo = (c.W + 2 * o.pad - o.k) / o.s + 1;
+        c.cout = o.cout;
+        c.k = o.k;
+        c.s = o.s;
+        c.pad = o.pad;
+        c.act = o.act;
+        c.kpad = kpad_of(o);
+        c.K = o.k * o.k * o.cin;
+        c.M = B * c.Ho * c.Wo;
+        c.w = wb + o.w_off;
+        c.bias = reinterpret_cast<const float*>(wb + o.b_off);
+        if (o.kind == YV7_OP_CONV) {
+          const auto& to = p->tensors[o.dst];
+          if (c.Ho != (H >> to.shift) || c.Wo != (W >> to.shift))
+            return fail(YV7_E_SHAPE, "yv7_forward: op " + std::to_string(i) + " output shape mismatch");
+          c.y = wsb + off[o.dst];
+          c.yc = to.channels;
+          c.yoff = o.dst_coff;
+          e = yv7::launch_conv(p->dtype, c, false, st);
+        } else {
+          c.z = z;
+          c.raw = raw ? raw + raw_off[o.level] : nullptr;
+          c.nrows = nrows;
+          c.row_off = row_off[o.level];
+          c.na = p->na;
+          c.no = p->no;
+          c.stride = p->stride[o.level];
+          for (int a = 0; a < p->na * 2; ++a) c.anchor[a] = p->anchor_grid[o.level * p->na * 2 + a];
+          e = yv7::launch_conv(p->dtype, c, true, st);
+        }
+        break;
+      }
+      case YV7_OP_MAXPOOL: {
+        const auto& ti = p->tensors[o.src];
+        const auto& to = p->tensors[o.dst];
+        const int Hi = H >> ti.shift, Wi = W >> ti.shift;
+        const int Ho = (Hi + 2 * o.pad - o.k) / o.s + 1, Wo = (Wi + 2 * o.pad - o.k) / o.s + 1;
+        if (Ho != (H >> to.shift) || Wo != (W >> to.shift))
+          return fail(YV7_E_SHAPE, "yv7_forward: maxpool op " + std::to_string(i) + " shape mismatch");
+        e = yv7::launch_maxpool(p->dtype, wsb + off[o.src], B, Hi, Wi, ti.channels, o.src_coff, wsb + off[o.dst], Ho,
+                                Wo, to.channels, o.dst_coff, o.cout, o.k, o.s, o.pad, st);
+        break;
+      }
+      case YV7_OP_UPSAMPLE: {
+        const auto& ti = p->tensors[o.src];
+        const auto& to = p->tensors[o.dst];
+        if (to.shift + 1 != ti.shift) return fail(YV7_E_SHAPE, "yv7_forward: upsample shift mismatch");
+        e = yv7::launch_upsample2x(p->dtype, wsb + off[o.src], B, H >> ti.shift, W >> ti.shift, ti.channels,
+                                   o.src_coff, wsb + off[o.dst], to.channels, o.dst_coff, o.cout, st);
+        break;
+      }
+      case YV7_OP_COPY: {
+        const auto& ti = p->tensors[o.src];
+        const auto& to = p->tensors[o.dst];
+        if (to.shift != ti.shift) return fail(YV7_E_SHAPE, "yv7_forward: copy shift mismatch");
+        e = yv7::launch_copy(p->dtype, wsb + off[o.src], B, H >> ti.shift, W >> ti.shift, ti.channels, o.src_coff,
+                             wsb + off[o.dst], to.channels, o.dst_coff, o.cout, st);
+        break;
+      }
+      default:
+        return fail(YV7_E_ARG, "yv7_forward: unknown op kind");
+    }
+    if (e != hipSuccess) return hip_fail(e, "yv7_forward launch");
+  }
+  (void)es;
+  return 0;
+}
+
+size_t yv7_nms_workspace_bytes(int B, int N, int no, int multi_label, int max_nms) {
+  if (B <= 0 || N <= 0 || no < 6 || max_nms <= 0) return 0;
+  return yv7::nms_workspace_bytes(B, N, no, multi_label, max_nms);
+}
+
+static int nms_check(const float* z, int B, int N, int no, int max_det, int max_nms, void* ws, size_t ws_bytes,
+                     int multi) {
+  if (!z || !ws) return fail(YV7_E_ARG, "yv7_nms: null argument");
+  if (B <= 0 || N <= 0 || no < 6 || no - 5 > 128) return fail(YV7_E_SHAPE, "yv7_nms: bad z shape (nc <= 128)");
+  if (max_det <= 0 || max_nms <= 0 || max_nms > 65536) return fail(YV7_E_ARG, "yv7_nms: max_det/max_nms out of range");
+  if (ws_bytes < yv7::nms_workspace_bytes(B, N, no, multi, max_nms)) return fail(YV7_E_WORKSPACE, "yv7_nms: workspace too small");
+  return 0;
+}
+
+int yv7_nms(const float* z, int B, int N, int no, float conf_thres, float iou_thres, int multi_label, int agnostic,
+            const int32_t* classes, int ncls, int max_det, int max_nms, float* det, int64_t* src_row, int32_t* count,
+            void* ws, size_t ws_bytes, void* stream) {
+  if (int rc = nms_check(z, B, N, no, max_det, max_nms, ws, ws_bytes, multi_label)) return rc;
+  if (!det || !src_row || !count || (ncls > 0 && !classes)) return fail(YV7_E_ARG, "yv7_nms: null output");
+  hipError_t e = yv7::launch_nms(z, B, N, no, conf_thres, iou_thres, multi_label, agnostic, 0,
+                                 ncls > 0 ? classes : nullptr, ncls, max_det, max_nms, det, src_row, count, ws,
+                                 reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "yv7_nms");
+  return 0;
+}
+
+static const int E2E_MAX_NMS = 65536;
+
+static size_t e2e_layout(int B, int N, int no, int topk, size_t* det_off, size_t* src_off, size_t* cnt_off) {
+  const size_t need = yv7::nms_workspace_bytes(B, N, no, 1, E2E_MAX_NMS);
+  *det_off = align256(need);
+  *src_off = align256(*det_off + sizeof(float) * 6 * (size_t)B * topk);
+  *cnt_off = align256(*src_off + sizeof(int64_t) * (size_t)B * topk);
+  return align256(*cnt_off + sizeof(int32_t) * (size_t)B);
+}
+
+size_t yv7_end2end_workspace_bytes(int B, int N, int no, int topk) {
+  if (B <= 0 || N <= 0 || no < 6 || topk <= 0) return 0;
+  size_t a, b, c;
+  return e2e_layout(B, N, no, topk, &a, &b, &c);
+}
+
+int yv7_end2end(const float* z, int B, int N, int no, float conf_thres, float iou_thres, int topk, int32_t* num_dets,
+                float* det_boxes, float* det_scores, int32_t* det_classes, void* ws, size_t ws_bytes, void* stream) {
+  // multi-label candidates, class-aware IoU on raw boxes (EfficientNMS), top-k by score
+  const int max_nms = E2E_MAX_NMS;
+  if (topk <= 0) return fail(YV7_E_ARG, "yv7_end2end: topk must be positive");
+  if (B <= 0 || N <= 0 || no < 6 || no - 5 > 128) return fail(YV7_E_SHAPE, "yv7_end2end: bad z shape");
+  size_t det_off, src_off, cnt_off;
+  const size_t total = e2e_layout(B, N, no, topk, &det_off, &src_off, &cnt_off);
+  if (!z || !ws || !num_dets || !det_boxes || !det_scores || !det_classes) return fail(YV7_E_ARG, "yv7_end2end: null");
+  if (ws_bytes < total) return fail(YV7_E_WORKSPACE, "yv7_end2end: workspace too small (need " + std::to_string(total) + ")");
+  unsigned char* w = reinterpret_cast<unsigned char*>(ws);
+  float* det = reinterpret_cast<float*>(w + det_off);
+  int64_t* src = reinterpret_cast<int64_t*>(w + src_off);
+  int32_t* cnt = reinterpret_cast<int32_t*>(w + cnt_off);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  hipError_t e = yv7::launch_nms(z, B, N, no, conf_thres, iou_thres, 1, 0, 1, nullptr, 0, topk, max_nms, det, src,
+                                 cnt, ws, st);
+  if (e != hipSuccess) return hip_fail(e, "yv7_end2end nms");
+  e = yv7::launch_end2end_pack(det, cnt, B, topk, topk, num_dets, det_boxes, det_scores, det_classes, st);
+  if (e != hipSuccess) return hip_fail(e, "yv7_end2end pack");
+  return 0;
+}
+
+}  // extern "C"

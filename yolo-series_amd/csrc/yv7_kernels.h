@@ -1,0 +1,44 @@
+// Shared definitions of the yv7 HIP kernels (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace yv7 {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+
+// Elements of T per 16-byte vector.
+template <typename T> struct Vec;
+template <> struct Vec<_Float16> { static constexpr int N = 8; };
+template <> struct Vec<float> { static constexpr int N = 4; };
+
+// Kernel parameters of one conv launch (also the fused Detect head).
+struct ConvParams {
+  const void* x;      // NHWC input tensor base
+  void* y;            // NHWC output tensor base (CONV)
+  const void* w;      // packed weights [cout_pad][kpad]
+  const float* bias;  // [cout_pad]
+  int B, H, W, xc, xoff, cin;       // input geometry, pitch (channels), channel offset, channels read
+  int Ho, Wo, yc, yoff, cout;       // output geometry
+  int k, s, pad, act, kpad, K, M;   // K = k*k*cin, M = B*Ho*Wo
+  // Detect epilogue
+  float* z;           // [B, N, no] fp32
+  float* raw;         // [B, na, Ho, Wo, no] fp32 for this level (nullable)
+  int nrows, row_off, na, no;
+  float stride, anchor[8];  // anchor[2*a + {0,1}] pixels
+};
+
+// Host launchers (defined in the .hip files, called from the runtime).
+hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t st);
+hipError_t launch_input(int dtype, const void* x, int x_dtype, void* y, int B, int H, int W, int yc,
+                        bool reorg, hipStream_t st);
+hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int Ho,
+                          int Wo, int yc, int yoff, int C, int k, int s, int pad, hipStream_t st);
+hipError_t launch_upsample2x(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int yc,
+                             int yoff, int C, hipStream_t st);
+hipError_t launch_copy(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int yc, int yoff,
+                       int C, hipStream_t st);
+
+}  // namespace yv7

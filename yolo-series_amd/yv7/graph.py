@@ -1,0 +1,296 @@
+"""Graph compiler: a models.yolo.Model -> the flat libyv7 plan (NHWC tensors, ops, packed weights).
+
+Walks the parsed layer list the way forward_once does (models/yolo.py:601-631) and emits one op per
+kernel launch:
+  Conv / RepConv           -> CONV (BN / RepVGG branches folded in fp32 first, Model.fuse arithmetic)
+  SPPCSPC                  -> 7 CONV + 3 MAXPOOL(5) cascaded (5, 5∘5 = 9, 5∘5∘5 = 13: max is associative and
+                              the -inf padding clips identically), concats as channel slices (common.py:276-280)
+  MP / SP                  -> MAXPOOL(k, k, 0) / MAXPOOL(k, s, k//2)
+  nn.Upsample(x2 nearest)  -> UPSAMPLE
+  Concat                   -> nothing: producers write their channel slice of the concat tensor directly;
+                              an input that already lives in another concat (or is the input image) gets a COPY
+  ReOrg at layer 0         -> fused into the INPUT packing op (space-to-depth while converting NCHW -> NHWC)
+  Detect / IDetect / IAuxDetect -> one DETECT op per level (1x1 conv + bias + sigmoid + decode -> z)
+Layers whose outputs never reach the head (IAuxDetect's auxiliary branch) are not emitted.
+
+Weights: each conv's fused W [cout, cin, k, k] becomes [cout_pad32][k][k][cin_pad] (K padded to 32) in the
+plan dtype, bias fp32 [cout_pad32]; every blob entry 256-byte aligned.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+
+import torch
+import torch.nn as nn
+
+from models.common import MP, SP, SPPCSPC, Concat, Conv, ReOrg, RepConv
+from models.yolo import Detect
+from yv7 import _lib as L
+
+
+@dataclass
+class Graph:
+    dtype: int
+    tensors: list = field(default_factory=list)   # [channels, shift]
+    ops: list = field(default_factory=list)       # dicts of OpDesc fields
+    blobs: list = field(default_factory=list)     # (offset, uint8 tensor)
+    nbytes: int = 0
+    nl: int = 0
+    na: int = 0
+    no: int = 0
+    stride: list = None
+    anchor_grid: list = None
+    max_shift: int = 0
+    layer_tensor: dict = field(default_factory=dict)   # layer i -> (tensor, coff, channels) for debugging
+    flops_per_pixel: float = 0.0                       # conv MACs*2 per input pixel (for roofline accounting)
+
+    def add_tensor(self, channels, shift):
+        self.tensors.append([channels, shift])
+        return len(self.tensors) - 1
+
+    def add_blob(self, t: torch.Tensor):
+        b = t.contiguous().view(torch.uint8).reshape(-1).cpu()
+        off = self.nbytes
+        self.blobs.append((off, b))
+        self.nbytes = (off + b.numel() + 255) // 256 * 256
+        return off
+
+    def weight_blob(self):
+        out = torch.zeros(max(self.nbytes, 1), dtype=torch.uint8)
+        for off, b in self.blobs:
+            out[off:off + b.numel()] = b
+        return out
+
+
+def _vec(dtype):
+    return 8 if dtype == L.DT_F16 else 4
+
+
+def _rup(x, m):
+    return (x + m - 1) // m * m
+
+
+def _act_code(act):
+    if isinstance(act, nn.SiLU):
+        return L.ACT_SILU
+    if isinstance(act, nn.LeakyReLU):
+        if abs(act.negative_slope - 0.1) > 1e-12:
+            raise NotImplementedError('LeakyReLU slope other than 0.1')
+        return L.ACT_LEAKY
+    if isinstance(act, nn.Identity):
+        return L.ACT_NONE
+    raise NotImplementedError(f'activation {type(act).__name__}')
+
+
+def _pack_conv(g: Graph, w: torch.Tensor, b: torch.Tensor, cin_pad: int):
+    """fp32 W [cout, cin, k, k] -> [cout_pad32][k*k*cin_pad -> K padded to 32] (plan dtype); bias fp32."""
+    cout, cin, k, _ = w.shape
+    tdt = torch.float16 if g.dtype == L.DT_F16 else torch.float32
+    wk = w.permute(0, 2, 3, 1)  # [cout, k, k, cin]
+    if cin_pad != cin:
+        wk = torch.nn.functional.pad(wk, [0, cin_pad - cin])
+    wk = wk.reshape(cout, -1)
+    kpad = _rup(k * k * cin_pad, 32)
+    cpad = _rup(cout, 32)
+    wp = torch.zeros(cpad, kpad, dtype=torch.float32)
+    wp[:cout, :wk.shape[1]] = wk
+    bp = torch.zeros(cpad, dtype=torch.float32)
+    bp[:cout] = b
+    w_off = g.add_blob(wp.to(tdt))
+    b_off = g.add_blob(bp)
+    return w_off, b_off
+
+
+def _live_layers(layers, nl):
+    """Layers whose output reaches the Detect head (drops IAuxDetect's auxiliary branch)."""
+    n = len(layers)
+    need = [False] * n
+    need[n - 1] = True
+    for i in range(n - 1, -1, -1):
+        if not need[i]:
+            continue
+        m = layers[i]
+        srcs = [m.f] if isinstance(m.f, int) else list(m.f)
+        if isinstance(m, Detect):
+            srcs = srcs[:nl]
+        for j in srcs:
+            jj = i + j if j < 0 else j
+            if jj >= 0:
+                need[jj] = True
+    return need
+
+
+def compile_model(model, dtype: int) -> Graph:
+    layers = list(model.model)
+    det = layers[-1]
+    if not isinstance(det, Detect):
+        raise NotImplementedError('the last layer must be a Detect / IDetect / IAuxDetect head')
+    V = _vec(dtype)
+    g = Graph(dtype=dtype, nl=det.nl, na=det.na, no=det.no)
+    g.stride = [float(s) for s in det.stride]
+    g.anchor_grid = det.anchor_grid.detach().float().cpu().reshape(-1).tolist()
+    live = _live_layers(layers, det.nl)
+
+    def absf(i, f):
+        return i + f if f < 0 else f
+
+    # ---- pass 1: output channels and spatial shift of every layer
+    ch, shift = {}, {}
+    c_in, s_in = model.yaml.get('ch', 3), 0
+    for m in layers:
+        i = m.i
+        srcs = [m.f] if isinstance(m.f, int) else list(m.f)
+        prev = [absf(i, j) for j in srcs]
+        pc = [c_in if j < 0 else ch[j] for j in prev]
+        ps = [s_in if j < 0 else shift[j] for j in prev]
+        if isinstance(m, Conv):
+            ch[i], shift[i] = m.conv.out_channels, ps[0] + (1 if m.conv.stride[0] == 2 else 0)
+        elif isinstance(m, RepConv):
+            c = m.rbr_reparam if hasattr(m, 'rbr_reparam') else m.rbr_dense[0]
+            ch[i], shift[i] = c.out_channels, ps[0] + (1 if c.stride[0] == 2 else 0)
+        elif isinstance(m, SPPCSPC):
+            ch[i], shift[i] = m.cv7.conv.out_channels, ps[0]
+        elif isinstance(m, MP):
+            ch[i], shift[i] = pc[0], ps[0] + 1
+        elif isinstance(m, SP):
+            ch[i], shift[i] = pc[0], ps[0]
+        elif isinstance(m, nn.Upsample):
+            if m.mode != 'nearest' or float(m.scale_factor) != 2.0:
+                raise NotImplementedError('only nn.Upsample(scale_factor=2, mode="nearest")')
+            ch[i], shift[i] = pc[0], ps[0] - 1
+        elif isinstance(m, ReOrg):
+            if i != 0:
+                raise NotImplementedError('ReOrg is supported as the first layer (fused into input packing)')
+            ch[i], shift[i] = pc[0] * 4, ps[0] + 1
+        elif isinstance(m, Concat):
+            if len(set(ps)) != 1:
+                raise ValueError(f'layer {i}: concat of different resolutions')
+            ch[i], shift[i] = sum(pc), ps[0]
+        elif isinstance(m, Detect):
+            ch[i], shift[i] = 0, 0
+        else:
+            raise NotImplementedError(f'layer {i}: {type(m).__name__}')
+    g.max_shift = max(shift.values())
+
+    # ---- tensor 0: the packed network input (INPUT op; ReOrg at layer 0 is fused into it)
+    loc = {}        # layer -> (tensor, coff)
+    reorg0 = isinstance(layers[0], ReOrg)
+    if c_in != 3:
+        raise NotImplementedError('the input packing op handles 3-channel images')
+    in_c = 12 if reorg0 else 3
+    t_in = g.add_tensor(_rup(in_c, V), 1 if reorg0 else 0)
+    g.ops.append(dict(kind=L.OP_INPUT, src=-1, dst=t_in, k=2 if reorg0 else 1, cout=in_c))
+    if reorg0:
+        loc[0] = (t_in, 0)
+
+    # ---- pass 2: concat placement (producers write straight into the concat tensor)
+    placeable = (Conv, RepConv, SPPCSPC, MP, SP, nn.Upsample)
+    placed = set()
+    for m in layers:
+        if isinstance(m, Concat) and live[m.i]:
+            t = g.add_tensor(_rup(ch[m.i], V), shift[m.i])
+            loc[m.i] = (t, 0)
+            off = 0
+            for j in m.f:
+                jj = absf(m.i, j)
+                if jj >= 0 and jj not in loc and isinstance(layers[jj], placeable) and ch[jj] % V == 0 and off % V == 0:
+                    loc[jj] = (t, off)
+                    placed.add((jj, m.i))
+                off += ch[jj] if jj >= 0 else c_in
+
+
+    def src_of(i, j):
+        jj = absf(i, j)
+        if jj < 0:
+            return t_in, 0, in_c
+        t, off = loc[jj]
+        return t, off, ch[jj]
+
+    def out_of(i):
+        if i not in loc:
+            loc[i] = (g.add_tensor(_rup(ch[i], V), shift[i]), 0)
+        return loc[i]
+
+    def conv_op(src, dst, w, b, k, s, pad, act):
+        (ts, so, cs), (td, do) = src, dst
+        cin_pad = _rup(cs, V)
+        if cin_pad != cs and g.tensors[ts][0] < so + cin_pad:
+            raise ValueError('channel padding would read outside the source tensor')
+        w_off, b_off = _pack_conv(g, w, b, cin_pad)
+        g.ops.append(dict(kind=L.OP_CONV, src=ts, src_coff=so, cin=cin_pad, dst=td, dst_coff=do, cout=w.shape[0],
+                          k=k, s=s, pad=pad, act=act, w_off=w_off, b_off=b_off))
+
+    for m in layers:
+        i = m.i
+        if not live[i] or (reorg0 and i == 0):
+            continue
+        if isinstance(m, (Conv, RepConv)):
+            w, b = m.fused_weight_bias()
+            c = m.conv if isinstance(m, Conv) else (m.rbr_reparam if hasattr(m, 'rbr_reparam') else m.rbr_dense[0])
+            if c.groups != 1 or c.dilation[0] != 1:
+                raise NotImplementedError('grouped / dilated conv')
+            conv_op(src_of(i, m.f), out_of(i), w, b, c.kernel_size[0], c.stride[0], c.padding[0], _act_code(m.act))
+        elif isinstance(m, SPPCSPC):
+            src = src_of(i, m.f)
+            c_ = m.cv1.conv.out_channels
+            s = shift[i]
+            t1 = g.add_tensor(_rup(c_, V), s)
+            t3 = g.add_tensor(_rup(c_, V), s)
+            cat1 = g.add_tensor(_rup(4 * c_, V), s)
+            t5 = g.add_tensor(_rup(c_, V), s)
+            cat2 = g.add_tensor(_rup(2 * c_, V), s)
+            if c_ % V:
+                raise NotImplementedError('SPPCSPC hidden width must be a multiple of the vector width')
+
+            def cv(mod, a, d):
+                w, b = mod.fused_weight_bias()
+                k = mod.conv.kernel_size[0]
+                conv_op(a, d, w, b, k, 1, k // 2, _act_code(mod.act))
+
+            cv(m.cv1, src, (t1, 0))
+            cv(m.cv3, (t1, 0, c_), (t3, 0))
+            cv(m.cv4, (t3, 0, c_), (cat1, 0))
+            ks = [p.kernel_size for p in m.m]
+            if ks == [5, 9, 13]:  # cascade: pool9 = pool5(pool5), pool13 = pool5(pool9)
+                for q in range(3):
+                    g.ops.append(dict(kind=L.OP_MAXPOOL, src=cat1, src_coff=q * c_, dst=cat1, dst_coff=(q + 1) * c_,
+                                      cout=c_, k=5, s=1, pad=2))
+            else:
+                for q, k in enumerate(ks):
+                    g.ops.append(dict(kind=L.OP_MAXPOOL, src=cat1, src_coff=0, dst=cat1, dst_coff=(q + 1) * c_,
+                                      cout=c_, k=k, s=1, pad=k // 2))
+            cv(m.cv5, (cat1, 0, 4 * c_), (t5, 0))
+            cv(m.cv6, (t5, 0, c_), (cat2, 0))
+            cv(m.cv2, src, (cat2, c_))
+            cv(m.cv7, (cat2, 0, 2 * c_), out_of(i))
+        elif isinstance(m, (MP, SP)):
+            (ts, so, cs), (td, do) = src_of(i, m.f), out_of(i)
+            p = m.m
+            k = p.kernel_size if isinstance(p.kernel_size, int) else p.kernel_size[0]
+            st = p.stride if isinstance(p.stride, int) else p.stride[0]
+            pd = p.padding if isinstance(p.padding, int) else p.padding[0]
+            g.ops.append(dict(kind=L.OP_MAXPOOL, src=ts, src_coff=so, dst=td, dst_coff=do, cout=cs, k=k, s=st, pad=pd))
+        elif isinstance(m, nn.Upsample):
+            (ts, so, cs), (td, do) = src_of(i, m.f), out_of(i)
+            g.ops.append(dict(kind=L.OP_UPSAMPLE, src=ts, src_coff=so, dst=td, dst_coff=do, cout=cs))
+        elif isinstance(m, Concat):
+            t, _ = loc[i]
+            off = 0
+            for j in m.f:
+                jj = absf(i, j)
+                cs_ = ch[jj] if jj >= 0 else in_c
+                if (jj, i) not in placed:
+                    ts, so, cs = src_of(i, j)
+                    if cs % V or off % V:
+                        raise NotImplementedError('concat slice not a multiple of the vector width')
+                    g.ops.append(dict(kind=L.OP_COPY, src=ts, src_coff=so, dst=t, dst_coff=off, cout=cs))
+                off += cs_
+        elif isinstance(m, Detect):
+            for lvl in range(m.nl):
+                ts, so, cs = src_of(i, m.f[lvl])
+                w, b = m.head_weights(lvl)
+                w_off, b_off = _pack_conv(g, w, b, _rup(cs, V))
+                g.ops.append(dict(kind=L.OP_DETECT, src=ts, src_coff=so, cin=_rup(cs, V), dst=-1, cout=w.shape[0],
+                                  k=1, s=1, pad=0, level=lvl, w_off=w_off, b_off=b_off))
+    g.layer_tensor = {i: (loc[i][0], loc[i][1], ch[i]) for i in loc}
+    return g

@@ -1,0 +1,130 @@
+"""Plan: a compiled network resident on one MI355X, driven through the C ABI (libyv7).
+
+Plan.from_model(model, device, dtype) compiles the model (yv7.graph), packs its weights once and
+creates the libyv7 plan on that device (weights copied into plan-owned HBM).  Plan.forward(x)
+allocates nothing after the first call for a given (B, H, W): the workspace and outputs are cached,
+and the whole network is one yv7_forward call on the current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import torch
+
+from yv7 import _lib as L
+from yv7.graph import compile_model
+
+
+class Plan:
+    def __init__(self, graph, device, weights: torch.Tensor):
+        self.graph = graph
+        self.device = torch.device(device)
+        self.dtype = graph.dtype
+        self.nl, self.na, self.no = graph.nl, graph.na, graph.no
+        lib = L.lib()
+        self._tensors = (L.TensorDesc * len(graph.tensors))(*[L.TensorDesc(c, s) for c, s in graph.tensors])
+        ops = []
+        for o in graph.ops:
+            d = dict(kind=0, src=0, src_coff=0, cin=0, dst=0, dst_coff=0, cout=0, k=1, s=1, pad=0, act=0, level=0,
+                     w_off=0, b_off=0)
+            d.update(o)
+            ops.append(L.OpDesc(**d))
+        self._ops = (L.OpDesc * len(ops))(*ops)
+        self._stride = (ctypes.c_float * graph.nl)(*graph.stride)
+        self._anchors = (ctypes.c_float * len(graph.anchor_grid))(*graph.anchor_grid)
+        desc = L.NetDesc(L.ABI_VERSION, graph.dtype, len(graph.tensors), self._tensors, len(ops), self._ops,
+                         graph.nl, graph.na, graph.no, self._stride, self._anchors, graph.max_shift)
+        self._desc = desc
+        h = ctypes.c_void_p()
+        dev_index = self.device.index if self.device.index is not None else torch.cuda.current_device()
+        with torch.cuda.device(dev_index):
+            L.check(lib.yv7_plan_create(ctypes.byref(desc), weights.data_ptr(), weights.numel(), dev_index,
+                                        ctypes.byref(h)), 'yv7_plan_create')
+        self._h = h
+        self._ws = {}
+        self.weight_bytes = weights.numel()
+
+    @classmethod
+    def from_model(cls, model, device, dtype=torch.float32, weights=None):
+        code = L.DT_F16 if dtype == torch.float16 else L.DT_F32
+        g = compile_model(model, code)
+        blob = g.weight_blob() if weights is None else weights
+        blob = blob.to(device)
+        return cls(g, device, blob)
+
+    def __del__(self):
+        h = getattr(self, '_h', None)
+        if h is not None and h.value:
+            try:
+                L.lib().yv7_plan_destroy(h)
+            except Exception:
+                pass
+
+    # ------------------------------------------------------------------
+    def num_rows(self, H, W):
+        return int(L.lib().yv7_num_rows(self._h, H, W))
+
+    def workspace(self, B, H, W):
+        key = (B, H, W)
+        ws = self._ws.get(key)
+        if ws is None:
+            nbytes = L.lib().yv7_workspace_bytes(self._h, B, H, W)
+            if nbytes == 0:
+                L.check(-2, f'yv7_workspace_bytes(B={B}, H={H}, W={W})')
+            self._ws.clear()  # keep one shape resident
+            ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
+            self._ws[key] = ws
+        return ws
+
+    def tensor_view(self, tensor_id, B, H, W):
+        """NHWC view of an intermediate activation tensor of the last forward (debug / per-layer parity)."""
+        off = ctypes.c_int64()
+        dims = (ctypes.c_int64 * 4)()
+        L.check(L.lib().yv7_tensor_info(self._h, tensor_id, B, H, W, ctypes.byref(off), dims), 'yv7_tensor_info')
+        ws = self.workspace(B, H, W)
+        es = 2 if self.dtype == L.DT_F16 else 4
+        n = dims[0] * dims[1] * dims[2] * dims[3]
+        t = ws[off.value:off.value + n * es].view(torch.float16 if es == 2 else torch.float32)
+        return t.view(dims[0], dims[1], dims[2], dims[3])
+
+    def layer_output(self, layer_i, B, H, W):
+        """NCHW fp32 copy of layer `layer_i`'s output from the last forward."""
+        t, coff, c = self.graph.layer_tensor[layer_i]
+        return self.tensor_view(t, B, H, W)[..., coff:coff + c].permute(0, 3, 1, 2).float().contiguous()
+
+    def forward_into(self, x, z, raw=None, stream=None):
+        B, C, H, W = x.shape
+        if C != 3:
+            raise ValueError(f'expected a [B,3,H,W] image batch, got {tuple(x.shape)}')
+        if x.dtype not in (torch.float32, torch.float16):
+            x = x.float()
+        x = x.contiguous()
+        ws = self.workspace(B, H, W)
+        xdt = L.DT_F16 if x.dtype == torch.float16 else L.DT_F32
+        if stream is None:
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        rc = L.lib().yv7_forward(self._h, x.data_ptr(), xdt, B, H, W, z.data_ptr(),
+                                 raw.data_ptr() if raw is not None else None, ws.data_ptr(), ws.numel(), stream)
+        L.check(rc, 'yv7_forward')
+
+    def forward(self, x, want_raw=True):
+        """x [B,3,H,W] on the plan's device -> (z [B,N,no] fp32, xs: list of [B,na,ny,nx,no] fp32)."""
+        if x.device != self.device and not (self.device.index is None and x.is_cuda):
+            raise RuntimeError(f'input on {x.device}, plan on {self.device}')
+        B, _, H, W = x.shape
+        N = self.num_rows(H, W)
+        if N <= 0:
+            L.check(-2, f'yv7_num_rows(H={H}, W={W})')
+        z = torch.empty((B, N, self.no), dtype=torch.float32, device=x.device)
+        raw = torch.empty((B * N * self.no,), dtype=torch.float32, device=x.device) if want_raw else None
+        self.forward_into(x, z, raw)
+        xs = None
+        if want_raw:
+            xs, o = [], 0
+            for lvl in range(self.nl):
+                s = int(self.graph.stride[lvl])
+                ny, nx = H // s, W // s
+                n = B * self.na * ny * nx * self.no
+                xs.append(raw[o:o + n].view(B, self.na, ny, nx, self.no))
+                o += n
+        return z, xs
