@@ -103,6 +103,13 @@ int64_t yv7_num_rows(const yv7_plan* plan, int H, int W);
 int yv7_forward(yv7_plan* plan, const void* x, int x_dtype, int B, int H, int W, float* z_out,
                 float* raw_out, void* workspace, size_t ws_bytes, void* stream);
 
+/* Live per-op timing: with max_forwards > 0 every following yv7_forward (up to max_forwards of
+ * them) records one HIP event before its first op and one after each op on its stream; 0 turns it
+ * off and frees the events.  yv7_profile_read synchronizes on the recorded events and returns, per
+ * op, the elapsed milliseconds summed over the recorded forwards (op_ms: [n_ops]). */
+int yv7_profile_enable(yv7_plan* plan, int max_forwards);
+int yv7_profile_read(yv7_plan* plan, int* n_forwards, float* op_ms);
+
 /* Byte offset of activation tensor `tensor_id` inside the forward workspace and its NHWC dims
  * [B, H', W', channels] — lets a caller read any intermediate layer for per-layer parity checks. */
 int yv7_tensor_info(const yv7_plan* plan, int tensor_id, int B, int H, int W, int64_t* offset,

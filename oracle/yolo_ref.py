@@ -286,10 +286,24 @@ def detect_decode(net: Net, raw: list):
     return torch.cat(z, 1), xs
 
 
-def forward(net: Net, fused: dict, x: torch.Tensor, return_all=False):
-    """forward_once (models/yolo.py:601-631) on the fused (deploy) network; returns (z, xs)."""
+def _half_round(v):
+    if isinstance(v, tuple):
+        return (v[0].half().float(), v[1].half().float())
+    if isinstance(v, dict):
+        return {j: _half_round(t) for j, t in v.items()}
+    return [_half_round(t) for t in v]
+
+
+def forward(net: Net, fused: dict, x: torch.Tensor, return_all=False, half_storage=False):
+    """forward_once (models/yolo.py:601-631) on the fused (deploy) network; returns (z, xs).
+
+    half_storage=True emulates the reference's GPU half() path (detect.py:48-49,101): weights, the
+    input and every layer output rounded to fp16, arithmetic (conv accumulation) in fp32."""
     y = []
     outs = {}
+    if half_storage:
+        fused = {k: _half_round(v) for k, v in fused.items()}
+        x = x.half().float()
     for L in net.layers:
         if L.f != -1:
             x = y[L.f] if isinstance(L.f, int) else [x if j == -1 else y[j] for j in L.f]
@@ -299,10 +313,11 @@ def forward(net: Net, fused: dict, x: torch.Tensor, return_all=False):
         elif t == 'SPPCSPC':
             cv = fused[L.i]
             silu = ('silu',)
-            x1 = _conv(_conv(_conv(x, cv[1], 1, 1, 0, silu), cv[3], 3, 1, 1, silu), cv[4], 1, 1, 0, silu)
+            r = (lambda t: t.half().float()) if half_storage else (lambda t: t)
+            x1 = r(_conv(r(_conv(r(_conv(x, cv[1], 1, 1, 0, silu)), cv[3], 3, 1, 1, silu)), cv[4], 1, 1, 0, silu))
             cat = torch.cat([x1] + [F.max_pool2d(x1, k, 1, k // 2) for k in L.p['pools']], 1)
-            y1 = _conv(_conv(cat, cv[5], 1, 1, 0, silu), cv[6], 3, 1, 1, silu)
-            y2 = _conv(x, cv[2], 1, 1, 0, silu)
+            y1 = r(_conv(r(_conv(cat, cv[5], 1, 1, 0, silu)), cv[6], 3, 1, 1, silu))
+            y2 = r(_conv(x, cv[2], 1, 1, 0, silu))
             x = _conv(torch.cat((y1, y2), dim=1), cv[7], 1, 1, 0, silu)
         elif t == 'MP':
             x = F.max_pool2d(x, L.p['k'], L.p['k'])
@@ -319,7 +334,30 @@ def forward(net: Net, fused: dict, x: torch.Tensor, return_all=False):
             x = detect_decode(net, raw)
         else:
             raise NotImplementedError(t)
+        if half_storage and isinstance(x, torch.Tensor):
+            x = x.half().float()
         if return_all:
             outs[L.i] = x
         y.append(x if L.i in net.save else None)
     return (x, outs) if return_all else x
+
+
+def forward64(net: Net, fused: dict, x: torch.Tensor):
+    """The same restatement evaluated in float64 — the accuracy yardstick for fp32 parity tolerances:
+    a different fp32 summation order (another BLAS, ISA or thread count) legitimately moves the
+    reference's own fp32 z by about |z32 - z64|."""
+    def d(v):
+        if isinstance(v, tuple):
+            return (v[0].double(), v[1].double())
+        if isinstance(v, dict):
+            return {j: d(t) for j, t in v.items()}
+        return [d(t) for t in v]
+
+    f64 = {k: d(v) for k, v in fused.items()}
+    ag = net.anchor_grid
+    net.anchor_grid = ag.double()
+    try:
+        z, xs = forward(net, f64, x.double())
+    finally:
+        net.anchor_grid = ag
+    return z, xs

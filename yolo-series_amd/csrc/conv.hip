@@ -39,11 +39,15 @@ __device__ __forceinline__ void mfma_step<_Float16>(const u4& a, const u4& b, f4
 template <>
 __device__ __forceinline__ void mfma_step<float>(const u4& a, const u4& b, f4& acc) {
   // lane group g = lane>>4 holds k = 4g..4g+3 of this step; MFMA kk consumes k = 4g+kk from A and B.
+  // Blocked summation: the step's 16 products are summed in a fresh accumulator and then added to
+  // the running total, so the fp32 rounding error grows with K/16 + 16 instead of K (parity mode).
   const f4 fa = __builtin_bit_cast(f4, a), fb = __builtin_bit_cast(f4, b);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[0], fb[0], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[1], fb[1], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[2], fb[2], acc, 0, 0, 0);
-  acc = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[3], fb[3], acc, 0, 0, 0);
+  f4 t = {0.f, 0.f, 0.f, 0.f};
+  t = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[0], fb[0], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[1], fb[1], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[2], fb[2], t, 0, 0, 0);
+  t = __builtin_amdgcn_mfma_f32_16x16x4f32(fa[3], fb[3], t, 0, 0, 0);
+  acc += t;
 }
 
 template <typename T, int BM, int BN, bool ONE, bool DET>

@@ -338,27 +338,25 @@ __global__ __launch_bounds__(SORT_T) void nms_greedy(const NmsArgs a) {
     if (threadIdx.x == 0) total += nk;
     __syncthreads();
     if (total >= a.max_det) break;
-    // strike later candidates overlapped by a box kept in this block
-    const int w0 = (base + 64) >> 5;
-    const int wend = (n + 31) >> 5;
+    // strike later candidates overlapped by a box kept in this block: one candidate per lane, each
+    // wave owns whole 64-candidate chunks (two bitmap words), so no atomics are needed
     if (nk > 0) {
-      for (int wi = w0 + threadIdx.x; wi < wend; wi += SORT_T) {
-        uint32_t word = removed[wi];
-        for (int bit = 0; bit < 32; ++bit) {
-          const int j = wi * 32 + bit;
-          if (j >= n || ((word >> bit) & 1u)) continue;
+      const int wv = threadIdx.x >> 6;
+      for (int c0 = base + 64 + wv * 64; c0 < n; c0 += (SORT_T / 64) * 64) {
+        const int j = c0 + lane;
+        bool hit = false;
+        if (j < n && !((removed[j >> 5] >> (j & 31)) & 1u)) {
           const float4 bj = sbox[j];
           const float aj = sarea[j];
           const int cj = a.per_class ? cand[order[j]].cls : -1;
-          for (int t = 0; t < nk; ++t) {
+          for (int t = 0; t < nk && !hit; ++t) {
             if (a.per_class && kcls[t] != cj) continue;
-            if (iou_gt(kbox[t], karea[t], bj, aj, a.iou)) {
-              word |= 1u << bit;
-              break;
-            }
+            hit = iou_gt(kbox[t], karea[t], bj, aj, a.iou);
           }
         }
-        removed[wi] = word;
+        const uint64_t hm = __ballot(hit);
+        if (lane == 0) removed[c0 >> 5] |= (uint32_t)hm;
+        if (lane == 32) removed[(c0 >> 5) + 1] |= (uint32_t)(hm >> 32);
       }
     }
     __syncthreads();

@@ -33,6 +33,9 @@ struct yv7_plan {
   std::vector<float> stride, anchor_grid;
   void* weights = nullptr;
   size_t wbytes = 0;
+  // live profiling: events[f * (n_ops + 1) + i]
+  std::vector<hipEvent_t> events;
+  int prof_max = 0, prof_used = 0;
 };
 
 namespace {
@@ -155,8 +158,51 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
   return 0;
 }
 
+static void free_events(yv7_plan* p) {
+  for (auto e : p->events) (void)hipEventDestroy(e);
+  p->events.clear();
+  p->prof_max = p->prof_used = 0;
+}
+
+int yv7_profile_enable(yv7_plan* p, int max_forwards) {
+  if (!p || max_forwards < 0) return fail(YV7_E_ARG, "yv7_profile_enable");
+  free_events(p);
+  if (max_forwards == 0) return 0;
+  const size_t n = (size_t)max_forwards * (p->ops.size() + 1);
+  p->events.resize(n);
+  for (size_t i = 0; i < n; ++i) {
+    hipError_t e = hipEventCreate(&p->events[i]);
+    if (e != hipSuccess) {
+      p->events.resize(i);
+      free_events(p);
+      return hip_fail(e, "hipEventCreate");
+    }
+  }
+  p->prof_max = max_forwards;
+  return 0;
+}
+
+int yv7_profile_read(yv7_plan* p, int* n_forwards, float* op_ms) {
+  if (!p || !n_forwards || !op_ms) return fail(YV7_E_ARG, "yv7_profile_read");
+  const size_t nops = p->ops.size();
+  for (size_t i = 0; i < nops; ++i) op_ms[i] = 0.f;
+  *n_forwards = p->prof_used;
+  for (int f = 0; f < p->prof_used; ++f) {
+    hipEvent_t* ev = &p->events[(size_t)f * (nops + 1)];
+    hipError_t e = hipEventSynchronize(ev[nops]);
+    if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
+    for (size_t i = 0; i < nops; ++i) {
+      float ms = 0.f;
+      if ((e = hipEventElapsedTime(&ms, ev[i], ev[i + 1])) != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+      op_ms[i] += ms;
+    }
+  }
+  return 0;
+}
+
 void yv7_plan_destroy(yv7_plan* p) {
   if (!p) return;
+  free_events(p);
   if (p->weights) (void)hipFree(p->weights);
   delete p;
 }
@@ -227,6 +273,12 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
     }
   }
   hipError_t e = hipSuccess;
+  hipEvent_t* ev = nullptr;
+  if (p->prof_used < p->prof_max) {
+    ev = &p->events[(size_t)p->prof_used * (p->ops.size() + 1)];
+    p->prof_used++;
+    if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+  }
   for (size_t i = 0; i < p->ops.size(); ++i) {
     const auto& o = p->ops[i];
     switch (o.kind) {
@@ -311,6 +363,7 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
         return fail(YV7_E_ARG, "yv7_forward: unknown op kind");
     }
     if (e != hipSuccess) return hip_fail(e, "yv7_forward launch");
+    if (ev && (e = hipEventRecord(ev[i + 1], st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
   (void)es;
   return 0;

@@ -1,0 +1,52 @@
+"""Batch sharding over the GPUs of one node: one process per GPU, torch.distributed over RCCL.
+
+Images are independent, so the data path needs no collective: rank r runs its own
+contiguous slice of the global batch through its own plan.  The two collectives are the ones the
+north star names:
+  * broadcast_weights: rank 0 packs the fused network once; the packed blob (73.9 MB fp16 for
+    yolov7) goes to every rank with one RCCL broadcast over xGMI, so every rank runs bit-identical
+    weights without re-folding them.
+  * gather_detections: the fixed-shape per-rank NMS outputs (det [b,300,6] fp32, src_row [b,300]
+    int64, count [b] int32) are all-gathered once per batch (~0.3 MB per rank for b = 32) so every
+    rank holds the detections of the whole global batch in global image order.
+"""
+from __future__ import annotations
+
+import torch
+import torch.distributed as dist
+
+from yv7.graph import compile_model
+from yv7.runtime import Plan
+from yv7 import _lib as L
+
+
+def shard(global_batch: int, rank: int, world: int):
+    """Contiguous slice [lo, hi) of the global batch owned by `rank` (images r*B/W ... (r+1)*B/W)."""
+    base, rem = divmod(global_batch, world)
+    lo = rank * base + min(rank, rem)
+    return lo, lo + base + (1 if rank < rem else 0)
+
+
+def broadcast_weights(model, device, dtype, group=None):
+    """Compile on every rank (cheap, host-only), pack on rank 0, RCCL-broadcast the packed blob."""
+    code = L.DT_F16 if dtype == torch.float16 else L.DT_F32
+    g = compile_model(model, code)
+    if dist.get_rank(group) == 0:
+        blob = g.weight_blob().to(device)
+    else:
+        blob = torch.empty(max(g.nbytes, 1), dtype=torch.uint8, device=device)
+    dist.broadcast(blob, src=0, group=group)
+    return Plan(g, device, blob)
+
+
+def gather_detections(det, src_row, count, group=None):
+    """All-gather fixed-shape per-rank NMS outputs -> global (det, src_row, count) in image order."""
+    world = dist.get_world_size(group)
+    if world == 1:
+        return det, src_row, count
+    outs = []
+    for t in (det, src_row, count):
+        o = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(o, t.contiguous(), group=group)
+        outs.append(o)
+    return tuple(outs)

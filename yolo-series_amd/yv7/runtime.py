@@ -92,6 +92,53 @@ class Plan:
         t, coff, c = self.graph.layer_tensor[layer_i]
         return self.tensor_view(t, B, H, W)[..., coff:coff + c].permute(0, 3, 1, 2).float().contiguous()
 
+    # ------------------------------------------------------------------ live per-op timing
+    def profile_enable(self, max_forwards):
+        L.check(L.lib().yv7_profile_enable(self._h, int(max_forwards)), 'yv7_profile_enable')
+
+    def profile_read(self):
+        """(number of recorded forwards, per-op milliseconds summed over them)."""
+        n = ctypes.c_int()
+        ms = (ctypes.c_float * len(self.graph.ops))()
+        L.check(L.lib().yv7_profile_read(self._h, ctypes.byref(n), ms), 'yv7_profile_read')
+        return n.value, list(ms)
+
+    def op_costs(self, B, H, W, x_bytes=4, with_raw=True):
+        """Per op: (kind, algorithmic FLOPs, algorithmic HBM bytes) for a [B,3,H,W] batch.
+
+        Bytes follow the layer-boundary model: every op reads its input slice once and
+        writes its output once, weights once per batch; concat costs nothing; the head writes z in
+        fp32 (and the raw logits, also fp32, which the reference returns as xs)."""
+        es = 2 if self.dtype == L.DT_F16 else 4
+        out = []
+        for o in self.graph.ops:
+            kind = o['kind']
+            if kind == L.OP_INPUT:
+                sh = self.graph.tensors[o['dst']][1]
+                npx = B * (H >> sh) * (W >> sh)
+                out.append((kind, 0.0, B * 3 * H * W * x_bytes + npx * self.graph.tensors[o['dst']][0] * es))
+                continue
+            si = self.graph.tensors[o['src']][1]
+            Hi, Wi = H >> si, W >> si
+            k, s, pad = o.get('k', 1), o.get('s', 1), o.get('pad', 0)
+            Ho, Wo = (Hi + 2 * pad - k) // s + 1, (Wi + 2 * pad - k) // s + 1
+            if kind in (L.OP_CONV, L.OP_DETECT):
+                cin, cout = o['cin'], o['cout']
+                flops = 2.0 * B * Ho * Wo * cout * k * k * cin
+                wbytes = cout * k * k * cin * es + cout * 4
+                obytes = B * Ho * Wo * cout * (es if kind == L.OP_CONV else (8 if with_raw else 4))
+                out.append((kind, flops, B * Hi * Wi * cin * es + obytes + wbytes))
+            elif kind == L.OP_MAXPOOL:
+                c = o['cout']
+                out.append((kind, 0.0, B * Hi * Wi * c * es + B * Ho * Wo * c * es))
+            elif kind == L.OP_UPSAMPLE:
+                c = o['cout']
+                out.append((kind, 0.0, B * Hi * Wi * c * es + B * 4 * Hi * Wi * c * es))
+            else:
+                c = o['cout']
+                out.append((kind, 0.0, 2 * B * Hi * Wi * c * es))
+        return out
+
     def forward_into(self, x, z, raw=None, stream=None):
         B, C, H, W = x.shape
         if C != 3:

@@ -43,9 +43,14 @@ def _act(m, x):
     return x
 
 
-def _calib_bn(gen, conv, bn, x):
+def _calib_bn(gen, conv, bn, x, gamma=(0.3, 0.6), beta_sd=0.7):
     """Seeded conv weight; BN running stats = this batch's per-channel statistics of the conv output
-    (what a training pass would have accumulated), jittered; returns the post-BN pre-activation tensor."""
+    (what a training pass would have accumulated), jittered; returns the post-BN pre-activation tensor.
+
+    gamma / beta: BN affine parameters U(gamma) / N(0, beta_sd).  Moderate gammas with larger betas
+    keep the random network well conditioned (fp32 vs fp64 box error ~1e-5 at 640, fp16-storage drift
+    ~1e-2), like a trained detector; gammas near 1 with small betas make a random 100-layer network
+    chaotic (fp32 vs fp64 ~1e-3, fp16 drift O(1)), which no trained YOLOv7 is."""
     co, ci, k, _ = conv.weight.shape
     bound = 1.0 / math.sqrt(ci * k * k)
     conv.weight.data = gen.uniform(conv.weight.shape, -bound, bound)
@@ -54,24 +59,46 @@ def _calib_bn(gen, conv, bn, x):
     var = y.var(dim=(0, 2, 3)) + 1e-6
     bn.running_mean.data = mean + gen.normal((co,), 0.0, 0.1) * var.sqrt()
     bn.running_var.data = var * gen.uniform((co,), 0.8, 1.25)
-    bn.weight.data = gen.uniform((co,), 0.8, 1.2)
-    bn.bias.data = gen.normal((co,), 0.0, 0.2)
+    bn.weight.data = gen.uniform((co,), gamma[0], gamma[1])
+    bn.bias.data = gen.normal((co,), 0.0, beta_sd)
     bn.num_batches_tracked.data = torch.tensor(1000)
     return F.batch_norm(y, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
 
 
-def _calib_conv(gen, m, x):
-    return _act(m, _calib_bn(gen, m.conv, m.bn, x))
+def _calib_conv(gen, m, x, **kw):
+    return _act(m, _calib_bn(gen, m.conv, m.bn, x, **kw))
+
+
+def _tune_head_biases(logits, na, no, target, conf=0.25):
+    """Shift class / objectness biases so that `target` of all anchor rows pass conf (obj*cls > conf)."""
+    rows = []
+    for lg in logits:  # [1, na*no, ny, nx] pre-bias logits + per-channel noise already added
+        v = lg.view(na, no, -1).permute(0, 2, 1).reshape(-1, no)
+        rows.append(v)
+    v = torch.cat(rows, 0)
+    mx = v[:, 5:].max(1).values
+    c_shift = -float(mx.median())            # the median row's best class logit sits at 0 (sigmoid 0.5)
+    cls = torch.sigmoid(mx + c_shift)
+    lo, hi = -20.0, 20.0
+    for _ in range(60):                      # bisection on the objectness shift
+        mid = 0.5 * (lo + hi)
+        frac = float(((torch.sigmoid(v[:, 4] + mid) > conf) & (torch.sigmoid(v[:, 4] + mid) * cls > conf))
+                     .float().mean())
+        lo, hi = (lo, mid) if frac > target else (mid, hi)
+    return 0.5 * (lo + hi), c_shift
 
 
 @torch.no_grad()
-def synthetic_state_dict(model, seed=0, head_gain=3.0, obj_bias=-2.5, cls_bias=-3.5, calib_hw=None):
+def synthetic_state_dict(model, seed=0, head_gain=2.0, target_candidates=0.06, calib_hw=None,
+                         gamma=(0.3, 0.6), beta_sd=0.7):
     """Fill `model` (unfused) in place with seeded synthetic weights and return its state_dict.
 
-    The BatchNorm statistics are estimated layer by layer on a small batch of synthetic frames
-    (1 x 3 x calib_hw x calib_hw), the way a training pass accumulates them; this is weight
+    The BatchNorm statistics are estimated layer by layer on one synthetic frame
+    (1 x 3 x calib_hw x calib_hw), the way a training pass accumulates them, and the head biases are
+    set so that `target_candidates` of the anchor rows pass conf 0.25 on that frame; this is weight
     synthesis only — inference never runs here."""
     gen = _Gen(seed)
+    bnkw = dict(gamma=gamma, beta_sd=beta_sd)
     layers = list(model.model)
     if calib_hw is None:  # the model's native resolution: 640 for P5, 1280 for P6 (max stride 64)
         calib_hw = 1280 if float(model.stride.max()) >= 64 else 640
@@ -83,10 +110,10 @@ def synthetic_state_dict(model, seed=0, head_gain=3.0, obj_bias=-2.5, cls_bias=-
         if m.f != -1:
             x = y[m.f] if isinstance(m.f, int) else [x if j == -1 else y[j] for j in m.f]
         if isinstance(m, Conv):
-            x = _calib_conv(gen, m, x)
+            x = _calib_conv(gen, m, x, **bnkw)
         elif isinstance(m, RepConv):
-            a = _calib_bn(gen, m.rbr_dense[0], m.rbr_dense[1], x)
-            b = _calib_bn(gen, m.rbr_1x1[0], m.rbr_1x1[1], x)
+            a = _calib_bn(gen, m.rbr_dense[0], m.rbr_dense[1], x, **bnkw)
+            b = _calib_bn(gen, m.rbr_1x1[0], m.rbr_1x1[1], x, **bnkw)
             if isinstance(m.rbr_identity, nn.BatchNorm2d):
                 bn = m.rbr_identity
                 bn.running_mean.data = x.mean(dim=(0, 2, 3))
@@ -96,11 +123,11 @@ def synthetic_state_dict(model, seed=0, head_gain=3.0, obj_bias=-2.5, cls_bias=-
                 a = a + F.batch_norm(x, bn.running_mean, bn.running_var, bn.weight, bn.bias, False, 0.0, bn.eps)
             x = _act(m, a + b)
         elif isinstance(m, SPPCSPC):
-            x1 = _calib_conv(gen, m.cv4, _calib_conv(gen, m.cv3, _calib_conv(gen, m.cv1, x)))
+            x1 = _calib_conv(gen, m.cv4, _calib_conv(gen, m.cv3, _calib_conv(gen, m.cv1, x, **bnkw), **bnkw), **bnkw)
             cat = torch.cat([x1] + [F.max_pool2d(x1, p.kernel_size, 1, p.kernel_size // 2) for p in m.m], 1)
-            y1 = _calib_conv(gen, m.cv6, _calib_conv(gen, m.cv5, cat))
-            y2 = _calib_conv(gen, m.cv2, x)
-            x = _calib_conv(gen, m.cv7, torch.cat((y1, y2), 1))
+            y1 = _calib_conv(gen, m.cv6, _calib_conv(gen, m.cv5, cat, **bnkw), **bnkw)
+            y2 = _calib_conv(gen, m.cv2, x, **bnkw)
+            x = _calib_conv(gen, m.cv7, torch.cat((y1, y2), 1), **bnkw)
         elif isinstance(m, MP):
             x = F.max_pool2d(x, m.m.kernel_size, m.m.stride)
         elif isinstance(m, SP):
@@ -113,16 +140,22 @@ def synthetic_state_dict(model, seed=0, head_gain=3.0, obj_bias=-2.5, cls_bias=-
             x = torch.cat([x[..., ::2, ::2], x[..., 1::2, ::2], x[..., ::2, 1::2], x[..., 1::2, 1::2]], 1)
         elif isinstance(m, Detect):
             feats = x if isinstance(x, list) else [x]
+            logits, noise = [], []
             for j, conv in enumerate(m.m):
                 c = conv.weight.shape[1]
                 bound = head_gain / math.sqrt(c)
                 w = gen.uniform(conv.weight.shape, -bound, bound)
                 conv.weight.data = w
+                lg = F.conv2d(feats[j], w)
                 # centre every head output on its own bias: remove the mean the features induce
-                mu = F.conv2d(feats[j], w).mean(dim=(0, 2, 3))
-                b = (gen.normal((m.na * m.no,), 0.0, 0.3) - mu).view(m.na, m.no)
-                b[:, 4] += obj_bias
-                b[:, 5:] += cls_bias
+                b = gen.normal((m.na * m.no,), 0.0, 0.3) - lg.mean(dim=(0, 2, 3))
+                noise.append(b)
+                logits.append(lg + b[None, :, None, None])
+            o_shift, c_shift = _tune_head_biases(logits, m.na, m.no, target_candidates)
+            for j, conv in enumerate(m.m):
+                b = noise[j].view(m.na, m.no).clone()
+                b[:, 4] += o_shift
+                b[:, 5:] += c_shift
                 conv.bias.data = b.reshape(-1)
             for conv in getattr(m, 'm2', []):
                 c = conv.weight.shape[1]
