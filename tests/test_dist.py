@@ -1,0 +1,75 @@
+"""Multi-process path on CPU (gloo, world_size 2): batch sharding, weight-blob broadcast, detection
+all-gather — the same yv7.dist code the 8-GPU bench runs over RCCL."""
+import os
+import socket
+
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from yv7.dist import gather_detections, shard
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, 'yolo-series_amd'), root, os.path.join(root, 'tests')]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from models.yolo import Model
+        from yv7 import _lib as L
+        from yv7.dist import gather_detections, shard
+        from yv7.graph import compile_model
+        from yv7.synthetic import synthetic_state_dict
+        # every rank builds the same synthetic weights; rank 0's packed blob is broadcast
+        m = Model('yolov7-tiny')
+        synthetic_state_dict(m, seed=0)
+        g = compile_model(m.float().fuse(), L.DT_F16)
+        mine = g.weight_blob()
+        blob = mine.clone() if rank == 0 else torch.zeros_like(mine)
+        dist.broadcast(blob, src=0)
+        same_blob = torch.equal(blob, mine)
+        # per-rank fixed-shape NMS outputs for its slice of a global batch of 6 images
+        lo, hi = shard(6, rank, world)
+        b = hi - lo
+        det = torch.arange(lo, hi, dtype=torch.float32).view(b, 1, 1).expand(b, 300, 6).contiguous()
+        src = torch.arange(lo, hi, dtype=torch.int64).view(b, 1).expand(b, 300).contiguous()
+        cnt = torch.arange(lo, hi, dtype=torch.int32)
+        gd, gs, gc = gather_detections(det, src, cnt)
+        q.put((rank, same_blob, gd[:, 0, 0].tolist(), gs[:, 0].tolist(), gc.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_shard_partition():
+    for B, W in [(256, 8), (32, 1), (10, 4), (3, 4)]:
+        parts = [shard(B, r, W) for r in range(W)]
+        assert parts[0][0] == 0 and parts[-1][1] == B
+        assert all(parts[i][1] == parts[i + 1][0] for i in range(W - 1))
+        assert max(h - l for l, h in parts) - min(h - l for l, h in parts) <= 1
+
+
+def test_gloo_world2_broadcast_and_gather():
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, same_blob, d, s, c in res:
+        assert same_blob
+        assert d == [0, 1, 2, 3, 4, 5] and s == [0, 1, 2, 3, 4, 5] and c == [0, 1, 2, 3, 4, 5]

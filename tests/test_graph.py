@@ -1,0 +1,62 @@
+"""Graph compiler: op lists, zero-copy concat placement, weight packing, algorithmic costs (CPU)."""
+import collections
+
+import pytest
+import torch
+
+from helpers import fresh_model
+from models.yolo import Model
+from yv7 import _lib as L
+from yv7.graph import _rup, compile_model
+
+
+@pytest.mark.parametrize('name', ['yolov7', 'yolov7-tiny', 'yolov7-w6', 'yolov7-train', 'yolov7-w6-train'])
+@pytest.mark.parametrize('dtype', [L.DT_F32, L.DT_F16])
+def test_compile_structure(name, dtype):
+    g = compile_model(Model(name), dtype)
+    V = 8 if dtype == L.DT_F16 else 4
+    kinds = collections.Counter(o['kind'] for o in g.ops)
+    assert kinds[L.OP_INPUT] == 1 and kinds[L.OP_DETECT] == g.nl
+    assert kinds[L.OP_COPY] == 0          # every concat of the yolov7 family is written in place
+    assert g.ops[0]['kind'] == L.OP_INPUT and g.ops[0]['dst'] == 0
+    for c, s in g.tensors:
+        assert c % V == 0 and 0 <= s <= g.max_shift
+    for o in g.ops:
+        if o['kind'] in (L.OP_CONV, L.OP_DETECT):
+            assert o['cin'] % V == 0 and o['w_off'] % 256 == 0 and o['b_off'] % 256 == 0
+            src_c = g.tensors[o['src']][0]
+            assert o['src_coff'] + o['cin'] <= src_c
+        if o['kind'] == L.OP_CONV:
+            assert o['dst_coff'] + o['cout'] <= g.tensors[o['dst']][0]
+
+
+def test_flops_match_baseline():
+    """Conv FLOPs per image at 640 (1280 for w6) equal BASELINE.md §2 (2*MAC, padded channels excluded)."""
+    from yv7.runtime import Plan
+    want = {'yolov7': (640, 104.51), 'yolov7-tiny': (640, 13.70), 'yolov7-w6': (1280, 359.72)}
+    for name, (hw, gflops) in want.items():
+        g = compile_model(Model(name), L.DT_F16)
+        p = Plan.__new__(Plan)
+        p.graph, p.dtype = g, g.dtype
+        tot = 0.0
+        for (kind, fl, by), o in zip(p.op_costs(1, hw, hw), g.ops):
+            if kind in (L.OP_CONV, L.OP_DETECT):
+                cin_real = 3 if o['src'] == 0 and not (g.ops[0]['k'] == 2) else (12 if o['src'] == 0 else o['cin'])
+                tot += fl * cin_real / o['cin']
+        assert tot / 1e9 == pytest.approx(gflops, rel=2e-3), name
+
+
+def test_weight_packing_round_trip():
+    m = fresh_model('yolov7-tiny')
+    g = compile_model(m, L.DT_F32)
+    blob = g.weight_blob()
+    layer1 = m.model[1]
+    w, b = layer1.fused_weight_bias()
+    op = [o for o in g.ops if o['kind'] == L.OP_CONV][1]   # op 0 is layer 0, op 1 is layer 1
+    cout, cin, k = w.shape[0], op['cin'], op['k']
+    kpad = _rup(k * k * cin, 32)
+    W = blob[op['w_off']:op['w_off'] + _rup(cout, 32) * kpad * 4].view(torch.float32).view(-1, kpad)
+    unpacked = W[:cout, :k * k * cin].view(cout, k, k, cin).permute(0, 3, 1, 2)
+    assert torch.equal(unpacked, w)
+    assert torch.equal(blob[op['b_off']:op['b_off'] + cout * 4].view(torch.float32), b)
+    assert torch.all(W[:, k * k * cin:] == 0) and torch.all(W[cout:] == 0)
