@@ -65,7 +65,7 @@ typedef struct {
   int32_t dst, dst_coff, cout; /* output tensor, channel offset, channels written */
   int32_t k, s, pad, act;      /* window / stride / padding / yv7_act */
   int32_t level;               /* DETECT: head level */
-  int64_t w_off;               /* CONV/DETECT: byte offset of weights [cout_pad][k][k][cin], K padded to 32 */
+  int64_t w_off;               /* CONV/DETECT: byte offset of weights [cout_pad32][k][k][cin], K padded to 64 */
   int64_t b_off;               /* CONV/DETECT: byte offset of fp32 bias [cout_pad] */
 } yv7_op_desc;
 

@@ -1,0 +1,47 @@
+"""Dev tool: per-op event timing of one plan forward (bs32 640 fp16 yolov7 by default) with rooflines."""
+import os, sys, argparse
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path[:0] = [os.path.join(ROOT, 'yolo-series_amd'), ROOT]
+import torch
+from models.yolo import Model
+from yv7.runtime import Plan
+from yv7.synthetic import synthetic_state_dict
+from yv7 import _lib as L
+ap = argparse.ArgumentParser(); ap.add_argument('--model', default='yolov7'); ap.add_argument('--b', type=int, default=32)
+ap.add_argument('--img', type=int, default=640); ap.add_argument('--dtype', default='f16'); ap.add_argument('--iters', type=int, default=10)
+a = ap.parse_args()
+dt = torch.float16 if a.dtype == 'f16' else torch.float32
+m = Model(a.model); synthetic_state_dict(m, seed=0); m = m.float().fuse().eval()
+plan = Plan.from_model(m, 'cuda:0', dt)
+B, H = a.b, a.img
+x = torch.rand(B, 3, H, H, device='cuda:0').to(dt)
+z = torch.empty(B, plan.num_rows(H, H), plan.no, device='cuda:0')
+for _ in range(3): plan.forward_into(x, z)
+torch.cuda.synchronize()
+plan.profile_enable(a.iters)
+for _ in range(a.iters): plan.forward_into(x, z)
+torch.cuda.synchronize()
+n, ms = plan.profile_read()
+costs = plan.op_costs(B, H, H, x_bytes=x.element_size(), with_raw=False)
+names = {0: 'INPUT', 1: 'CONV', 2: 'POOL', 3: 'UPS', 4: 'COPY', 5: 'DET'}
+tot = sum(ms) / n
+rows = []
+for i, ((kind, fl, by), t, o) in enumerate(zip(costs, ms, plan.graph.ops)):
+    t = t / n
+    sh = plan.graph.tensors[o['src']][1] if o['kind'] != 0 else 0
+    hw = H >> sh
+    desc = f"{names[kind]:5s} {o.get('cin',0):5d}->{o.get('cout',0):5d} k{o.get('k',1)} s{o.get('s',1)} @{hw}"
+    tf = fl / (t * 1e-3) / 1e12 if t > 0 else 0
+    gb = by / (t * 1e-3) / 1e9 if t > 0 else 0
+    # roofline-limited time at 8 TB/s and 2.5 PF
+    tmin = max(by / 8e12, fl / 2.5e15) * 1e3
+    rows.append((t, i, desc, tf, gb, tmin))
+print(f'forward {tot:.3f} ms over {n} forwards; sum of roofline minima {sum(r[5] for r in rows):.3f} ms')
+for t, i, desc, tf, gb, tmin in sorted(rows, reverse=True)[:40]:
+    print(f'{i:3d} {desc:32s} {t*1e3:8.1f} us  {tf:7.1f} TF/s  {gb:7.1f} GB/s  roof {tmin*1e3:7.1f} us  frac {tmin/t:5.2f}')
+by_kind = {}
+for t, i, desc, tf, gb, tmin in rows:
+    k = desc.split()[0] + (' k' + desc.split()[2][1] if desc.startswith('CONV') else '')
+    by_kind.setdefault(k, [0, 0, 0]); by_kind[k][0] += t; by_kind[k][1] += tmin; by_kind[k][2] += 1
+for k, (t, tm, c) in sorted(by_kind.items(), key=lambda kv: -kv[1][0]):
+    print(f'{k:10s} n={c:3d} {t:7.3f} ms roof {tm:7.3f} ms frac {tm/t:5.2f}')

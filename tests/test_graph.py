@@ -54,7 +54,7 @@ def test_weight_packing_round_trip():
     w, b = layer1.fused_weight_bias()
     op = [o for o in g.ops if o['kind'] == L.OP_CONV][1]   # op 0 is layer 0, op 1 is layer 1
     cout, cin, k = w.shape[0], op['cin'], op['k']
-    kpad = _rup(k * k * cin, 32)
+    kpad = _rup(k * k * cin, 64)
     W = blob[op['w_off']:op['w_off'] + _rup(cout, 32) * kpad * 4].view(torch.float32).view(-1, kpad)
     unpacked = W[:cout, :k * k * cin].view(cout, k, k, cin).permute(0, 3, 1, 2)
     assert torch.equal(unpacked, w)

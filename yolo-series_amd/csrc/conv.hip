@@ -13,6 +13,8 @@
 //   fp32: v_mfma_f32_16x16x4_f32 x4 per step: exact fp32 products, fp32 accumulate (parity mode).
 // Epilogue: + fp32 bias, SiLU / LeakyReLU(0.1) / none, convert, staged through LDS and stored as
 // 16-byte row chunks into a channel slice (offset yoff, pitch yc) of the output -> concat is free.
+#include <cstdlib>
+
 #include "yv7_kernels.h"
 
 namespace yv7 {
@@ -267,7 +269,13 @@ hipError_t launch_dt(const ConvParams& p, bool det, hipStream_t st) {
 }  // namespace
 
 hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t st) {
-  if (dtype == 1) return launch_dt<_Float16>(p, detect, st);
+  // fp16: the tuned kernel of conv_f16.hip (YV7_CONV_V1=1 selects this file's generic kernel, for A/B)
+  static const bool v1 = [] { const char* e = getenv("YV7_CONV_V1"); return e && e[0] == '1'; }();
+  // cout <= 32 (the stem of every model, tiny's narrow layers): this kernel's BK=32 steps waste less
+  // of the short, padded K than the 64-deep steps of conv_f16 (measured: scripts/convbench.hip)
+  if (dtype == 1)
+    return (v1 || p.variant == 1 || (p.variant == 0 && !detect && p.cout <= 32)) ? launch_dt<_Float16>(p, detect, st)
+                                                                                 : launch_conv_f16(p, detect, st);
   return launch_dt<float>(p, detect, st);
 }
 

@@ -33,6 +33,7 @@ struct yv7_plan {
   std::vector<float> stride, anchor_grid;
   void* weights = nullptr;
   size_t wbytes = 0;
+  void* zero = nullptr;  // 4 KiB of zeros: source of LDS-DMA loads for padding taps / out-of-range rows
   // live profiling: events[f * (n_ops + 1) + i]
   std::vector<hipEvent_t> events;
   int prof_max = 0, prof_used = 0;
@@ -77,7 +78,7 @@ int check_hw(const yv7_plan* p, int B, int H, int W) {
   return 0;
 }
 
-int kpad_of(const yv7_op_desc& o) { return (o.k * o.k * o.cin + 31) / 32 * 32; }
+int kpad_of(const yv7_op_desc& o) { return (o.k * o.k * o.cin + 63) / 64 * 64; }
 
 }  // namespace
 
@@ -154,6 +155,11 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
       return hip_fail(e, "hipMemcpy(weights)");
     }
   }
+  if ((e = hipMalloc(&p->zero, 4096)) != hipSuccess || (e = hipMemset(p->zero, 0, 4096)) != hipSuccess) {
+    if (p->weights) (void)hipFree(p->weights);
+    delete p;
+    return hip_fail(e, "hipMalloc(zero page)");
+  }
   *out = p;
   return 0;
 }
@@ -204,6 +210,7 @@ void yv7_plan_destroy(yv7_plan* p) {
   if (!p) return;
   free_events(p);
   if (p->weights) (void)hipFree(p->weights);
+  if (p->zero) (void)hipFree(p->zero);
   delete p;
 }
 
@@ -311,6 +318,7 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
         c.M = B * c.Ho * c.Wo;
         c.w = wb + o.w_off;
         c.bias = reinterpret_cast<const float*>(wb + o.b_off);
+        c.zero = p->zero;
         if (o.kind == YV7_OP_CONV) {
           const auto& to = p->tensors[o.dst];
           if (c.Ho != (H >> to.shift) || c.Wo != (W >> to.shift))

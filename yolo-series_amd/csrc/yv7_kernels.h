@@ -20,6 +20,7 @@ struct ConvParams {
   void* y;            // NHWC output tensor base (CONV)
   const void* w;      // packed weights [cout_pad][kpad]
   const float* bias;  // [cout_pad]
+  const void* zero;   // >= 16 zero bytes in device memory (LDS-DMA source for padding / out-of-range)
   int B, H, W, xc, xoff, cin;       // input geometry, pitch (channels), channel offset, channels read
   int Ho, Wo, yc, yoff, cout;       // output geometry
   int k, s, pad, act, kpad, K, M;   // K = k*k*cin, M = B*Ho*Wo
@@ -28,10 +29,12 @@ struct ConvParams {
   float* raw;         // [B, na, Ho, Wo, no] fp32 for this level (nullable)
   int nrows, row_off, na, no;
   float stride, anchor[8];  // anchor[2*a + {0,1}] pixels
+  int variant;        // 0 = tuned dispatch; >0 forces a kernel variant (microbenchmarks / A-B tests)
 };
 
 // Host launchers (defined in the .hip files, called from the runtime).
 hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t st);
+hipError_t launch_conv_f16(const ConvParams& p, bool detect, hipStream_t st);
 hipError_t launch_input(int dtype, const void* x, int x_dtype, void* y, int B, int H, int W, int yc,
                         bool reorg, hipStream_t st);
 hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int Ho,

@@ -13,7 +13,7 @@ kernel launch:
   Detect / IDetect / IAuxDetect -> one DETECT op per level (1x1 conv + bias + sigmoid + decode -> z)
 Layers whose outputs never reach the head (IAuxDetect's auxiliary branch) are not emitted.
 
-Weights: each conv's fused W [cout, cin, k, k] becomes [cout_pad32][k][k][cin_pad] (K padded to 32) in the
+Weights: each conv's fused W [cout, cin, k, k] becomes [cout_pad32][k][k][cin_pad] (K padded to 64) in the
 plan dtype, bias fp32 [cout_pad32]; every blob entry 256-byte aligned.
 """
 from __future__ import annotations
@@ -83,14 +83,14 @@ def _act_code(act):
 
 
 def _pack_conv(g: Graph, w: torch.Tensor, b: torch.Tensor, cin_pad: int):
-    """fp32 W [cout, cin, k, k] -> [cout_pad32][k*k*cin_pad -> K padded to 32] (plan dtype); bias fp32."""
+    """fp32 W [cout, cin, k, k] -> [cout_pad32][k*k*cin_pad -> K padded to 64] (plan dtype); bias fp32."""
     cout, cin, k, _ = w.shape
     tdt = torch.float16 if g.dtype == L.DT_F16 else torch.float32
     wk = w.permute(0, 2, 3, 1)  # [cout, k, k, cin]
     if cin_pad != cin:
         wk = torch.nn.functional.pad(wk, [0, cin_pad - cin])
     wk = wk.reshape(cout, -1)
-    kpad = _rup(k * k * cin_pad, 32)
+    kpad = _rup(k * k * cin_pad, 64)
     cpad = _rup(cout, 32)
     wp = torch.zeros(cpad, kpad, dtype=torch.float32)
     wp[:cout, :wk.shape[1]] = wk
