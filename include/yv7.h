@@ -49,7 +49,8 @@ typedef enum {
   YV7_OP_MAXPOOL = 2,  /* max pool k, stride s, pad (implicit -inf padding) */
   YV7_OP_UPSAMPLE = 3, /* nearest-neighbour x2 */
   YV7_OP_COPY = 4,     /* channel-slice copy (concat input that could not be written in place) */
-  YV7_OP_DETECT = 5    /* 1x1 conv + bias + sigmoid + grid/anchor decode -> z rows, raw logits */
+  YV7_OP_DETECT = 5,   /* 1x1 conv + bias + sigmoid + grid/anchor decode -> z rows, raw logits */
+  YV7_OP_STEM = 6      /* fp16: image -> conv A (3->32, 3x3, stride s) -> conv B (32->64, 3x3, s2), A kept in LDS */
 } yv7_op_kind;
 
 /* One NHWC activation tensor of the plan: [B, H >> shift, W >> shift, channels]. Tensor 0 is the
@@ -67,6 +68,8 @@ typedef struct {
   int32_t level;               /* DETECT: head level */
   int64_t w_off;               /* CONV/DETECT: byte offset of weights [cout_pad32][k][k][cin], K padded to 64 */
   int64_t b_off;               /* CONV/DETECT: byte offset of fp32 bias [cout_pad] */
+  int32_t cout2, act2;         /* STEM: second conv's output channels / activation */
+  int64_t w2_off, b2_off;      /* STEM: second conv's weights / bias */
 } yv7_op_desc;
 
 typedef struct {

@@ -23,12 +23,12 @@ for _ in range(a.iters): plan.forward_into(x, z)
 torch.cuda.synchronize()
 n, ms = plan.profile_read()
 costs = plan.op_costs(B, H, H, x_bytes=x.element_size(), with_raw=False)
-names = {0: 'INPUT', 1: 'CONV', 2: 'POOL', 3: 'UPS', 4: 'COPY', 5: 'DET'}
+names = {0: 'INPUT', 1: 'CONV', 2: 'POOL', 3: 'UPS', 4: 'COPY', 5: 'DET', 6: 'STEM'}
 tot = sum(ms) / n
 rows = []
 for i, ((kind, fl, by), t, o) in enumerate(zip(costs, ms, plan.graph.ops)):
     t = t / n
-    sh = plan.graph.tensors[o['src']][1] if o['kind'] != 0 else 0
+    sh = plan.graph.tensors[o['src']][1] if o['kind'] not in (0, 6) else 0
     hw = H >> sh
     desc = f"{names[kind]:5s} {o.get('cin',0):5d}->{o.get('cout',0):5d} k{o.get('k',1)} s{o.get('s',1)} @{hw}"
     tf = fl / (t * 1e-3) / 1e12 if t > 0 else 0

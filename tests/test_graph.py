@@ -16,9 +16,11 @@ def test_compile_structure(name, dtype):
     g = compile_model(Model(name), dtype)
     V = 8 if dtype == L.DT_F16 else 4
     kinds = collections.Counter(o['kind'] for o in g.ops)
-    assert kinds[L.OP_INPUT] == 1 and kinds[L.OP_DETECT] == g.nl
+    assert kinds[L.OP_INPUT] + kinds[L.OP_STEM] == 1 and kinds[L.OP_DETECT] == g.nl
     assert kinds[L.OP_COPY] == 0          # every concat of the yolov7 family is written in place
-    assert g.ops[0]['kind'] == L.OP_INPUT and g.ops[0]['dst'] == 0
+    assert g.ops[0]['kind'] in (L.OP_INPUT, L.OP_STEM)
+    # the fused stem is used exactly for the fp16 plans of the P5 models (not for w6: ReOrg front end)
+    assert (kinds[L.OP_STEM] == 1) == (dtype == L.DT_F16 and 'w6' not in name)
     for c, s in g.tensors:
         assert c % V == 0 and 0 <= s <= g.max_shift
     for o in g.ops:
@@ -40,6 +42,8 @@ def test_flops_match_baseline():
         p.graph, p.dtype = g, g.dtype
         tot = 0.0
         for (kind, fl, by), o in zip(p.op_costs(1, hw, hw), g.ops):
+            if kind == L.OP_STEM:
+                tot += fl
             if kind in (L.OP_CONV, L.OP_DETECT):
                 cin_real = 3 if o['src'] == 0 and not (g.ops[0]['k'] == 2) else (12 if o['src'] == 0 else o['cin'])
                 tot += fl * cin_real / o['cin']

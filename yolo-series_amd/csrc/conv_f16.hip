@@ -192,38 +192,71 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   }
 
   // accumulator acc[j][i][e]: output channel n = n0 + wn*WTN + j*16 + g*4 + e, pixel m = m0 + wm*WTM + i*16 + li
-  if (DET) {
+  if constexpr (DET) {
+    // Detect head (models/yolo.py:52-57): stage logits + bias as fp32 [BM][BN] in LDS, then decode in
+    // z order — for every anchor, BM consecutive pixels are BM consecutive 85-float rows of z — so
+    // z (and raw) leave as fully coalesced 4-byte streams.  BN covers all na*no head channels.
+    constexpr int DPITCH = BN * 4 + 16;
+    static_assert(BM * DPITCH + BM * 16 <= LDS, "detect staging");
+    float* Ds = reinterpret_cast<float*>(smem);
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WTN + j * 16 + g * 4;
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WTM + i * 16 + li;
+        f4 v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] + ((n0 + col + e < p.cout) ? p.bias[n0 + col + e] : 0.0f);
+        *reinterpret_cast<f4*>(reinterpret_cast<unsigned char*>(Ds) + row * DPITCH + col * 4) = v;
+      }
+    }
+    // per-pixel table: z row of anchor 0 (int64), grid x / y
+    unsigned char* tab = smem + BM * DPITCH;
+    long long* zrow0 = reinterpret_cast<long long*>(tab);
+    float* gxs = reinterpret_cast<float*>(tab + BM * 8);
+    float* gys = gxs + BM;
     const int hw = p.Ho * p.Wo;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * WTM + i * 16 + li;
-      if (m >= p.M) continue;
-      const int b = m / hw, rem = m - b * hw;
-      const int gy = rem / p.Wo, gx = rem - gy * p.Wo;
-#pragma unroll
-      for (int j = 0; j < TN; ++j) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int n = n0 + wn * WTN + j * 16 + g * 4 + e;
-          if (n >= p.cout) continue;
-          const int a = n / p.no, o = n - a * p.no;
-          const float v = acc[j][i][e] + p.bias[n];
-          const float sg = 1.0f / (1.0f + expf(-v));
+    if (tid < BM) {
+      const int m = m0 + tid;
+      const int mm = m < p.M ? m : p.M - 1;
+      const int b = mm / hw, cell = mm - b * hw;
+      const int gy = cell / p.Wo, gx = cell - gy * p.Wo;
+      zrow0[tid] = m < p.M ? (long long)b * p.nrows + p.row_off + cell : -1;
+      gxs[tid] = (float)gx;
+      gys[tid] = (float)gy;
+    }
+    __syncthreads();
+    // thread t walks e = t, t + NT, ... over the [BM][no] elements of one anchor: pr = e / no, o = e % no
+    const int NO = p.no, step_pr = NT / NO, step_o = NT - step_pr * NO;
+    for (int a = 0; a < p.na; ++a) {
+      const float aw = p.anchor[2 * a], ah = p.anchor[2 * a + 1];
+      const long long aoff = (long long)a * hw;
+      int pr = tid / NO, o = tid - pr * NO;
+      for (; pr < BM;) {
+        const long long zr = zrow0[pr];
+        if (zr >= 0) {
+          const float v = *reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(Ds) + pr * DPITCH +
+                                                          (a * NO + o) * 4);
+          const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
           float out;
           if (o < 2) {
-            const float t = sg * 2.0f;
-            const float u = t - 0.5f;
-            out = (u + ((o == 0) ? (float)gx : (float)gy)) * p.stride;
+            out = (sg * 2.0f - 0.5f + (o == 0 ? gxs[pr] : gys[pr])) * p.stride;
           } else if (o < 4) {
-            const float t = sg * 2.0f;
-            out = (t * t) * p.anchor[2 * a + (o - 2)];
+            const float t2 = sg * 2.0f;
+            out = (t2 * t2) * (o == 2 ? aw : ah);
           } else {
             out = sg;
           }
-          const size_t cell = ((size_t)a * p.Ho + gy) * p.Wo + gx;
-          p.z[(((size_t)b * p.nrows + p.row_off + cell) * p.no) + o] = out;
-          if (p.raw) p.raw[(((size_t)b * p.na * hw) + cell) * p.no + o] = v;
+          p.z[(size_t)(zr + aoff) * NO + o] = out;
+          if (p.raw) {
+            const long long b = (zr - p.row_off) / p.nrows, cell = (zr - p.row_off) - b * p.nrows;
+            p.raw[((size_t)(b * p.na + a) * hw + cell) * NO + o] = v;
+          }
         }
+        o += step_o;
+        pr += step_pr;
+        if (o >= NO) { o -= NO; ++pr; }
       }
     }
     return;
@@ -516,7 +549,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (p.cout <= 64) return one ? launch_dma<256, 64, 4, true, false, 3>(p, st) : launch_dma<256, 64, 4, false, false, 3>(p, st);
     return one ? launch_dma<128, 128, 2, true, false, 3>(p, st) : launch_dma<128, 128, 2, false, false, 3>(p, st);
   }
-  if (det) return launch_t<128, 128, 2, true, true>(p, st);
+  if (det) return launch_t<64, 256, 1, true, true>(p, st);
   if (variant == 2) {  // tall tiles for narrow layers
     if (p.cout <= 32) return one ? launch_t<256, 32, 4, true, false>(p, st) : launch_t<256, 32, 4, false, false>(p, st);
     if (p.cout <= 64) return one ? launch_t<256, 64, 4, true, false>(p, st) : launch_t<256, 64, 4, false, false>(p, st);

@@ -104,7 +104,7 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
       return fail(YV7_E_ARG, "yv7_plan_create: tensor " + std::to_string(i) + " has bad channels/shift");
   for (int i = 0; i < d->n_ops; ++i) {
     const auto& o = d->ops[i];
-    const bool src_ok = o.kind == YV7_OP_INPUT || (o.src >= 0 && o.src < d->n_tensors);
+    const bool src_ok = o.kind == YV7_OP_INPUT || o.kind == YV7_OP_STEM || (o.src >= 0 && o.src < d->n_tensors);
     const bool dst_ok = o.kind == YV7_OP_DETECT || (o.dst >= 0 && o.dst < d->n_tensors);
     if (!src_ok || !dst_ok) return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " bad tensor id");
     if (o.kind == YV7_OP_CONV || o.kind == YV7_OP_DETECT) {
@@ -116,6 +116,16 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
         return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " weight range outside blob");
       if (o.kind == YV7_OP_DETECT && (o.level < 0 || o.level >= d->nl || o.cout != d->na * d->no || o.k != 1))
         return fail(YV7_E_ARG, "yv7_plan_create: bad detect op");
+    }
+    if (o.kind == YV7_OP_STEM) {
+      if (d->dtype != YV7_DT_F16 || !yv7::stem_supported(o.cin, o.cout, o.cout2, o.s) || o.k != 3 ||
+          o.dst_coff % vec || o.dst_coff + o.cout2 > d->tensors[o.dst].channels)
+        return fail(YV7_E_ARG, "yv7_plan_create: unsupported stem op");
+      const size_t wa = (size_t)o.cout * ((27 + 63) / 64 * 64) * 2, wb = (size_t)o.cout2 * ((9 * o.cout + 63) / 64 * 64) * 2;
+      if (o.w_off < 0 || o.w2_off < 0 || (size_t)o.w_off + wa > nbytes || (size_t)o.w2_off + wb > nbytes ||
+          (size_t)o.b_off + 4 * o.cout > nbytes || (size_t)o.b2_off + 4 * o.cout2 > nbytes)
+        return fail(YV7_E_ARG, "yv7_plan_create: stem weight range outside blob");
+      continue;
     }
     if (o.kind != YV7_OP_INPUT && o.kind != YV7_OP_DETECT) {
       const int src_c = d->tensors[o.src].channels, dst_c = d->tensors[o.dst].channels;
@@ -338,6 +348,30 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
           for (int a = 0; a < p->na * 2; ++a) c.anchor[a] = p->anchor_grid[o.level * p->na * 2 + a];
           e = yv7::launch_conv(p->dtype, c, true, st);
         }
+        break;
+      }
+      case YV7_OP_STEM: {
+        const auto& to = p->tensors[o.dst];
+        if ((H >> to.shift) != H / o.s / 2 || (W >> to.shift) != W / o.s / 2)
+          return fail(YV7_E_SHAPE, "yv7_forward: stem output shape mismatch");
+        yv7::StemParams sp;
+        sp.x = x;
+        sp.y = wsb + off[o.dst];
+        sp.wa = wb + o.w_off;
+        sp.ba = reinterpret_cast<const float*>(wb + o.b_off);
+        sp.wb = wb + o.w2_off;
+        sp.bb = reinterpret_cast<const float*>(wb + o.b2_off);
+        sp.B = B;
+        sp.H = H;
+        sp.W = W;
+        sp.yc = to.channels;
+        sp.yoff = o.dst_coff;
+        sp.kpad_a = (27 + 63) / 64 * 64;
+        sp.kpad_b = (9 * o.cout + 63) / 64 * 64;
+        sp.act_a = o.act;
+        sp.act_b = o.act2;
+        sp.sa = o.s;
+        e = yv7::launch_stem(sp, x_dtype, st);
         break;
       }
       case YV7_OP_MAXPOOL: {

@@ -1,0 +1,200 @@
+// Fused stem for gfx950: image packing + conv A (3 -> CA, 3x3, stride SA) + conv B (CA -> CB, 3x3,
+// stride 2), conv A's activations never leave LDS.
+//
+// Replaces, for the yolov7 / yolov7-tiny stems, the reference's first two Conv layers
+// (models/common.py:110-111 on cfg/deploy/yolov7.yaml:15-17, yolov7-tiny.yaml:14-16) and the input
+// tensor preparation of detect.py:100-104.  Unfused, conv A's output is the largest tensor of the
+// network (32 x 640 x 640 x 32 fp16 = 839 MB per batch of 32) and is written once and read back nine
+// times through L2 by conv B; fused, it exists only as a 17 x 33 x CA tile in LDS per block.
+//
+// Per 256-thread block: a TBY x TBX tile of conv B's output for one image.
+//   1. the NCHW image patch feeding it (PY x PX x 3, zero outside the image) -> LDS [PY][PX][4] fp16
+//   2. conv A on the MFMA: M = TAY*TAX A-pixels (16 per tile), N = CA, K = 27 (one 16x16x32 step,
+//      k = tap*3 + ci, zero-padded to 32), operands gathered from the patch; + bias + act, zeroed
+//      outside the image (conv B's zero padding), -> LDS [A-pixel][CA] with an 80-byte pitch
+//      (conflict-free ds_read_b128 for conv B's stride-2 access)
+//   3. conv B on the MFMA: M = TBY*TBX, N = CB, K = 9 taps x CA; each wave owns 16 output channels and
+//      holds their 9 taps of weight fragments in registers (loaded at entry, under the patch load)
+//   4. + bias + act -> LDS tile -> 16-byte NHWC stores into the destination channel slice.
+#include "yv7_kernels.h"
+
+namespace yv7 {
+
+namespace {
+
+constexpr int NT = 256;
+
+__device__ __forceinline__ float act_fast(float v, int act) {
+  if (act == 1) return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
+  if (act == 2) return v > 0.0f ? v : v * 0.1f;
+  return v;
+}
+
+template <typename S, int CA, int CB, int SA, int TBY, int TBX>
+__global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
+  constexpr int TAY = 2 * TBY + 1, TAX = 2 * TBX + 1;      // conv-A pixels feeding the tile
+  constexpr int PY = SA * (TAY - 1) + 3, PX = SA * (TAX - 1) + 3;
+  constexpr int NA = TAY * TAX;
+  constexpr int MA = (NA + 15) / 16;                         // conv-A m-tiles
+  constexpr int APITCH = CA * 2 + 16;                        // bytes per A-pixel (padded)
+  constexpr int PATCH = PY * PX * 8;                         // [PY][PX][4] halves
+  constexpr int ABUF = NA * APITCH;
+  constexpr int MB = TBY * TBX / 16;                         // conv-B m-tiles
+  constexpr int CPITCH = CB * 2 + 16;
+  constexpr int OUTB = TBY * TBX * CPITCH;
+  constexpr int LDS0 = (PATCH + ABUF + 15) / 16 * 16;
+  constexpr int LDS = LDS0 > OUTB ? LDS0 : OUTB;
+  static_assert(CB == 64 && CA == 32, "one wave per 16 output channels, one MFMA k-step per tap");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
+  _Float16* patch = reinterpret_cast<_Float16*>(smem);
+  unsigned char* abuf = smem + (PATCH + 15) / 16 * 16;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int HA = p.H / SA, WA = p.W / SA;          // conv-A output size
+  const int HB = HA / 2, WB = WA / 2;              // conv-B output size
+  const int tiles_x = (WB + TBX - 1) / TBX, tiles_y = (HB + TBY - 1) / TBY;
+  int t = blockIdx.x;
+  const int b = t / (tiles_x * tiles_y);
+  t -= b * tiles_x * tiles_y;
+  const int oy0 = (t / tiles_x) * TBY, ox0 = (t % tiles_x) * TBX;
+  const int ay0 = 2 * oy0 - 1, ax0 = 2 * ox0 - 1;
+  const int iy0 = SA * ay0 - 1, ix0 = SA * ax0 - 1;
+
+  // conv-B weight fragments of this wave's 16 output channels, all 9 taps (K = 32 per tap = CA)
+  u4 wfr[9];
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap)
+    wfr[tap] = *reinterpret_cast<const u4*>(reinterpret_cast<const _Float16*>(p.wb) +
+                                            (size_t)(wave * 16 + li) * p.kpad_b + tap * CA + g * 8);
+
+  // 1. image patch -> LDS (fp16, channel 3 zero)
+  const S* xb = reinterpret_cast<const S*>(p.x) + (size_t)b * 3 * p.H * p.W;
+  for (int i = tid; i < PY * PX; i += NT) {
+    const int py = i / PX, px = i - py * PX;
+    const int iy = iy0 + py, ix = ix0 + px;
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    h4 v = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
+    if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W) {
+      const size_t o = (size_t)iy * p.W + ix;
+      v[0] = (_Float16)(float)xb[o];
+      v[1] = (_Float16)(float)xb[o + (size_t)p.H * p.W];
+      v[2] = (_Float16)(float)xb[o + 2 * (size_t)p.H * p.W];
+    }
+    *reinterpret_cast<h4*>(patch + i * 4) = v;
+  }
+  // conv-A weights: two 16-row tiles per n-tile pair, K = 32 (k = tap*3 + ci, 27..31 zero)
+  constexpr int NAT = CA / 16;
+  u4 wa[NAT];
+#pragma unroll
+  for (int nt = 0; nt < NAT; ++nt)
+    wa[nt] = *reinterpret_cast<const u4*>(reinterpret_cast<const _Float16*>(p.wa) + (size_t)(nt * 16 + li) * p.kpad_a + g * 8);
+  // per-lane gather offsets of its 8 k values (in halves, relative to the A-pixel's patch origin)
+  int koff[8];
+#pragma unroll
+  for (int kk = 0; kk < 8; ++kk) {
+    const int k = g * 8 + kk;
+    const int tap = k / 3, ci = k - tap * 3, r = tap / 3, s = tap - r * 3;
+    koff[kk] = k < 27 ? ((r * PX + s) * 4 + ci) : -1;
+  }
+  __syncthreads();
+
+  // 2. conv A on MFMA -> abuf
+  for (int mt = wave; mt < MA; mt += 4) {
+    const int m = mt * 16 + li;
+    const int mc = m < NA ? m : NA - 1;
+    const int yl = mc / TAX, xl = mc - yl * TAX;
+    const int base = (SA * yl * PX + SA * xl) * 4;
+    typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+    h8v xv;
+#pragma unroll
+    for (int kk = 0; kk < 8; ++kk) xv[kk] = koff[kk] >= 0 ? patch[base + koff[kk]] : (_Float16)0.f;
+    const int ay = ay0 + yl, ax = ax0 + xl;
+    const bool inside = m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA;
+#pragma unroll
+    for (int nt = 0; nt < NAT; ++nt) {
+      f4 acc = {0.f, 0.f, 0.f, 0.f};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[nt]), xv, acc, 0, 0, 0);
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      h4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int n = nt * 16 + g * 4 + e;
+        o[e] = inside ? (_Float16)act_fast(acc[e] + p.ba[n], p.act_a) : (_Float16)0.f;
+      }
+      if (m < NA) *reinterpret_cast<h4*>(abuf + m * APITCH + (nt * 16 + g * 4) * 2) = o;
+    }
+  }
+  __syncthreads();
+
+  // 3. conv B: wave w owns output channels [16w, 16w+16) for every pixel of the tile; its 9 taps of
+  //    weight fragments were loaded at kernel entry (wfr), so no global load sits in this loop.
+  f4 acc[MB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i) acc[i] = f4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int tap = 0; tap < 9; ++tap) {
+    const int r = tap / 3, s = tap - r * 3;
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int mb = i * 16 + li;                          // conv-B pixel within the tile
+      const int ty = mb / TBX, tx = mb - ty * TBX;
+      const int ap = (2 * ty + r) * TAX + (2 * tx + s);    // conv-A pixel (local)
+      const u4 xa = *reinterpret_cast<const u4*>(abuf + ap * APITCH + g * 16);
+      acc[i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wfr[tap]), __builtin_bit_cast(h8, xa),
+                                                      acc[i], 0, 0, 0);
+    }
+  }
+  __syncthreads();
+
+  // 4. epilogue via LDS: lane holds 4 consecutive channels of one conv-B pixel
+  {
+    const int col = wave * 16 + g * 4;
+    float bias[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bias[e] = p.bb[col + e];
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int mb = i * 16 + li;
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      h4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (_Float16)act_fast(acc[i][e] + bias[e], p.act_b);
+      *reinterpret_cast<h4*>(smem + mb * CPITCH + col * 2) = o;
+    }
+  }
+  __syncthreads();
+  constexpr int CPR = CB * 2 / 16;
+  _Float16* y = reinterpret_cast<_Float16*>(p.y);
+  for (int c = tid; c < TBY * TBX * CPR; c += NT) {
+    const int mb = c / CPR, ch = c - mb * CPR;
+    const int ty = mb / TBX, tx = mb - ty * TBX;
+    const int oy = oy0 + ty, ox = ox0 + tx;
+    if (oy < HB && ox < WB)
+      *reinterpret_cast<u4*>(y + (((size_t)b * HB + oy) * WB + ox) * p.yc + p.yoff + ch * 8) =
+          *reinterpret_cast<const u4*>(smem + mb * CPITCH + ch * 16);
+  }
+}
+
+template <typename S, int CA, int CB, int SA>
+hipError_t stem_t(const StemParams& p, hipStream_t st) {
+  constexpr int TBY = 8, TBX = 16;
+  const int HB = p.H / SA / 2, WB = p.W / SA / 2;
+  const int nblk = p.B * ((HB + TBY - 1) / TBY) * ((WB + TBX - 1) / TBX);
+  hipLaunchKernelGGL((stem_kernel<S, CA, CB, SA, TBY, TBX>), dim3(nblk), dim3(NT), 0, st, p);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+bool stem_supported(int cin, int ca, int cb, int sa) {
+  return cin == 3 && ca == 32 && cb == 64 && (sa == 1 || sa == 2);
+}
+
+hipError_t launch_stem(const StemParams& p, int x_dtype, hipStream_t st) {
+  if (p.sa == 1)
+    return x_dtype == 1 ? stem_t<_Float16, 32, 64, 1>(p, st) : stem_t<float, 32, 64, 1>(p, st);
+  return x_dtype == 1 ? stem_t<_Float16, 32, 64, 2>(p, st) : stem_t<float, 32, 64, 2>(p, st);
+}
+
+}  // namespace yv7

@@ -32,6 +32,17 @@ struct ConvParams {
   int variant;        // 0 = tuned dispatch; >0 forces a kernel variant (microbenchmarks / A-B tests)
 };
 
+// Fused stem: image -> conv A (3 -> 32, 3x3, stride sa) -> conv B (32 -> 64, 3x3, stride 2).
+struct StemParams {
+  const void* x;        // [B,3,H,W] image (fp16 or fp32)
+  void* y;              // conv-B output tensor base (NHWC fp16)
+  const void* wa;       // conv-A weights [32][kpad_a] (k = tap*3 + ci)
+  const float* ba;
+  const void* wb;       // conv-B weights [64][kpad_b] (k = tap*32 + ci)
+  const float* bb;
+  int B, H, W, yc, yoff, kpad_a, kpad_b, act_a, act_b, sa;
+};
+
 // Host launchers (defined in the .hip files, called from the runtime).
 hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t st);
 hipError_t launch_conv_f16(const ConvParams& p, bool detect, hipStream_t st);
@@ -41,6 +52,8 @@ hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc,
                           int Wo, int yc, int yoff, int C, int k, int s, int pad, hipStream_t st);
 hipError_t launch_upsample2x(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int yc,
                              int yoff, int C, hipStream_t st);
+bool stem_supported(int cin, int ca, int cb, int sa);
+hipError_t launch_stem(const StemParams& p, int x_dtype, hipStream_t st);
 hipError_t launch_copy(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int yc, int yoff,
                        int C, hipStream_t st);
 

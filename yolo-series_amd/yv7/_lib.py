@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(_HERE, 'libyv7.so')
 ABI_VERSION = 1
 DT_F32, DT_F16 = 0, 1
 ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
-OP_INPUT, OP_CONV, OP_MAXPOOL, OP_UPSAMPLE, OP_COPY, OP_DETECT = 0, 1, 2, 3, 4, 5
+OP_INPUT, OP_CONV, OP_MAXPOOL, OP_UPSAMPLE, OP_COPY, OP_DETECT, OP_STEM = 0, 1, 2, 3, 4, 5, 6
 
 
 class TensorDesc(ctypes.Structure):
@@ -29,7 +29,9 @@ class OpDesc(ctypes.Structure):
                 ('dst', ctypes.c_int32), ('dst_coff', ctypes.c_int32), ('cout', ctypes.c_int32),
                 ('k', ctypes.c_int32), ('s', ctypes.c_int32), ('pad', ctypes.c_int32), ('act', ctypes.c_int32),
                 ('level', ctypes.c_int32),
-                ('w_off', ctypes.c_int64), ('b_off', ctypes.c_int64)]
+                ('w_off', ctypes.c_int64), ('b_off', ctypes.c_int64),
+                ('cout2', ctypes.c_int32), ('act2', ctypes.c_int32),
+                ('w2_off', ctypes.c_int64), ('b2_off', ctypes.c_int64)]
 
 
 class NetDesc(ctypes.Structure):

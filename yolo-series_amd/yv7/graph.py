@@ -18,6 +18,7 @@ plan dtype, bias fp32 [cout_pad32]; every blob entry 256-byte aligned.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass, field
 
 import torch
@@ -120,6 +121,26 @@ def _live_layers(layers, nl):
     return need
 
 
+def _stem_candidate(layers, dtype):
+    """Layers 0-1 = Conv(3->32, 3x3, s1|s2) -> Conv(32->64, 3x3, s2) with layer 0 read only by layer 1:
+    the yolov7 / yolov7-tiny stems, fused into one fp16 op (csrc/stem.hip).  YV7_NO_STEM=1 disables."""
+    if dtype != L.DT_F16 or os.environ.get('YV7_NO_STEM') == '1' or len(layers) < 3:
+        return None
+    l0, l1 = layers[0], layers[1]
+    if not (type(l0) is Conv and type(l1) is Conv and l1.f == -1):
+        return None
+    c0, c1 = l0.conv, l1.conv
+    if not (c0.in_channels == 3 and c0.out_channels == 32 and c0.kernel_size[0] == 3 and c0.stride[0] in (1, 2)
+            and c0.padding[0] == 1 and c1.out_channels == 64 and c1.kernel_size[0] == 3 and c1.stride[0] == 2
+            and c1.padding[0] == 1 and c0.groups == 1 and c1.groups == 1):
+        return None
+    for m in layers[2:]:
+        srcs = [m.f] if isinstance(m.f, int) else list(m.f)
+        if any((m.i + j if j < 0 else j) == 0 for j in srcs):
+            return None
+    return True
+
+
 def compile_model(model, dtype: int) -> Graph:
     layers = list(model.model)
     det = layers[-1]
@@ -178,8 +199,12 @@ def compile_model(model, dtype: int) -> Graph:
     if c_in != 3:
         raise NotImplementedError('the input packing op handles 3-channel images')
     in_c = 12 if reorg0 else 3
-    t_in = g.add_tensor(_rup(in_c, V), 1 if reorg0 else 0)
-    g.ops.append(dict(kind=L.OP_INPUT, src=-1, dst=t_in, k=2 if reorg0 else 1, cout=in_c))
+    stem = _stem_candidate(layers, dtype) if not reorg0 else None
+    if stem is None:
+        t_in = g.add_tensor(_rup(in_c, V), 1 if reorg0 else 0)
+        g.ops.append(dict(kind=L.OP_INPUT, src=-1, dst=t_in, k=2 if reorg0 else 1, cout=in_c))
+    else:  # layers 0-1 run as one fused op straight from the image; tensor 0 is an unused placeholder
+        t_in = g.add_tensor(V, g.max_shift)
     if reorg0:
         loc[0] = (t_in, 0)
 
@@ -222,7 +247,19 @@ def compile_model(model, dtype: int) -> Graph:
 
     for m in layers:
         i = m.i
-        if not live[i] or (reorg0 and i == 0):
+        if not live[i] or (reorg0 and i == 0) or (stem is not None and i == 0):
+            continue
+        if stem is not None and i == 1:
+            l0, l1 = layers[0], layers[1]
+            wa, ba = l0.fused_weight_bias()
+            wb, bb = l1.fused_weight_bias()
+            wa_off, ba_off = _pack_conv(g, wa, ba, 3)
+            wb_off, bb_off = _pack_conv(g, wb, bb, l1.conv.in_channels)
+            td, do = out_of(1)
+            g.ops.insert(0, dict(kind=L.OP_STEM, src=-1, cin=3, cout=l0.conv.out_channels, k=3,
+                                 s=l0.conv.stride[0], pad=1, act=_act_code(l0.act), w_off=wa_off, b_off=ba_off,
+                                 dst=td, dst_coff=do, cout2=l1.conv.out_channels, act2=_act_code(l1.act),
+                                 w2_off=wb_off, b2_off=bb_off))
             continue
         if isinstance(m, (Conv, RepConv)):
             w, b = m.fused_weight_bias()

@@ -26,7 +26,7 @@ class Plan:
         ops = []
         for o in graph.ops:
             d = dict(kind=0, src=0, src_coff=0, cin=0, dst=0, dst_coff=0, cout=0, k=1, s=1, pad=0, act=0, level=0,
-                     w_off=0, b_off=0)
+                     w_off=0, b_off=0, cout2=0, act2=0, w2_off=0, b2_off=0)
             d.update(o)
             ops.append(L.OpDesc(**d))
         self._ops = (L.OpDesc * len(ops))(*ops)
@@ -113,6 +113,15 @@ class Plan:
         out = []
         for o in self.graph.ops:
             kind = o['kind']
+            if kind == L.OP_STEM:
+                sa = o['s']
+                Ha, Wa = H // sa, W // sa
+                ca, cb = o['cout'], o['cout2']
+                flops = 2.0 * B * Ha * Wa * ca * 27 + 2.0 * B * (Ha // 2) * (Wa // 2) * cb * 9 * ca
+                # reference-boundary bytes of the two layers it replaces (input read, A write + read, B write)
+                by = B * 3 * H * W * x_bytes + 2 * B * Ha * Wa * ca * es + B * (Ha // 2) * (Wa // 2) * cb * es
+                out.append((kind, flops, by))
+                continue
             if kind == L.OP_INPUT:
                 sh = self.graph.tensors[o['dst']][1]
                 npx = B * (H >> sh) * (W >> sh)
