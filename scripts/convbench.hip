@@ -1,8 +1,12 @@
-// Dev microbenchmark: time the fp16 conv kernel variants on yolov7-shaped layers (bs 32).
+// Dev microbenchmark: time the fp16 conv kernel variants on yolov7-shaped layers (bs 32), random
+// operands, and check every variant's output against the default dispatch (variant 0).
 // build: hipcc --offload-arch=gfx950 -O2 scripts/convbench.hip -I yolo-series_amd/csrc
-//        -L yolo-series_amd/yv7 -lyv7 -Wl,-rpath,$PWD/yolo-series_amd/yv7 -o convbench
+//        -L yolo-series_amd/yv7 -lyv7 -Wl,-rpath,$PWD/yolo-series_amd/yv7 -o scripts/convbench
+// usage: convbench [variant ...]      (default: 0 4 5)
 #include <hip/hip_runtime.h>
+#include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 #include "yv7_kernels.h"
@@ -11,53 +15,88 @@
 
 struct Shape { const char* name; int B, H, W, cin, cout, k, s; };
 
+__global__ void fill_rand(_Float16* p, size_t n, uint32_t seed, float scale) {
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    uint32_t h = (uint32_t)i * 2654435761u ^ seed;
+    h ^= h >> 15; h *= 2246822519u; h ^= h >> 13; h *= 3266489917u; h ^= h >> 16;
+    p[i] = (_Float16)(((h & 0xffff) / 32768.0f - 1.0f) * scale);
+  }
+}
+
 int main(int argc, char** argv) {
   std::vector<Shape> shapes = {
-    {"1x1 256->256 @160", 32, 160, 160, 256, 256, 1, 1},
+    {"3x3 64->64 @320", 32, 320, 320, 64, 64, 3, 1},
     {"3x3 64->64 @160", 32, 160, 160, 64, 64, 3, 1},
+    {"3x3 128->128 @80", 32, 80, 80, 128, 128, 3, 1},
     {"3x3 256->256 @40", 32, 40, 40, 256, 256, 3, 1},
-    {"1x1 1024->1024 @40", 32, 40, 40, 1024, 1024, 1, 1},
-    {"3x3 512->1024 @20", 32, 20, 20, 512, 1024, 3, 1},
+    {"3x3 512->512 @20", 32, 20, 20, 512, 512, 3, 1},
     {"3x3s2 128->128 @160", 32, 160, 160, 128, 128, 3, 2},
-    {"3x3 8->32 @640", 32, 640, 640, 8, 32, 3, 1},
+    {"3x3 128->256 @80", 32, 80, 80, 128, 256, 3, 1},
+    {"3x3 512->1024 @20", 32, 20, 20, 512, 1024, 3, 1},
+    {"1x1 256->256 @160", 32, 160, 160, 256, 256, 1, 1},
+    {"1x1 128->64 @160", 32, 160, 160, 128, 64, 1, 1},
+    {"1x1 512->512 @80", 32, 80, 80, 512, 512, 1, 1},
+    {"1x1 1024->1024 @40", 32, 40, 40, 1024, 1024, 1, 1},
     {"GEMM 4096^2 K4096", 32, 32, 32, 4096, 4096, 1, 1},
   };
-  int variants[] = {1, 2, 4};
+  std::vector<int> variants;
+  for (int i = 1; i < argc; ++i) variants.push_back(atoi(argv[i]));
+  if (variants.empty()) variants = {0, 4, 5};
   size_t maxx = 0, maxy = 0, maxw = 0;
   for (auto& s : shapes) {
-    maxx = std::max(maxx, (size_t)s.B * s.H * s.W * s.cin * 2);
-    maxy = std::max(maxy, (size_t)s.B * (s.H / s.s) * (s.W / s.s) * s.cout * 2);
-    maxw = std::max(maxw, (size_t)((s.cout + 31) / 32 * 32) * ((s.k * s.k * s.cin + 63) / 64 * 64) * 2);
+    maxx = std::max(maxx, (size_t)s.B * s.H * s.W * s.cin);
+    maxy = std::max(maxy, (size_t)s.B * (s.H / s.s) * (s.W / s.s) * s.cout);
+    maxw = std::max(maxw, (size_t)((s.cout + 31) / 32 * 32) * ((s.k * s.k * s.cin + 63) / 64 * 64));
   }
-  void *x, *y, *w, *b, *zero;
-  CK(hipMalloc(&x, maxx)); CK(hipMalloc(&y, maxy)); CK(hipMalloc(&w, maxw)); CK(hipMalloc(&b, 8192 * 4));
-  CK(hipMalloc(&zero, 4096)); CK(hipMemset(zero, 0, 4096));
-  CK(hipMemset(x, 0x3c, maxx)); CK(hipMemset(w, 0x1c, maxw)); CK(hipMemset(b, 0, 8192 * 4));
+  _Float16 *x, *y, *y0, *w;
+  float* b;
+  void* zero;
+  CK(hipMalloc(&x, maxx * 2)); CK(hipMalloc(&y, maxy * 2)); CK(hipMalloc(&y0, maxy * 2)); CK(hipMalloc(&w, maxw * 2));
+  CK(hipMalloc(&b, 8192 * 4)); CK(hipMalloc(&zero, 4096)); CK(hipMemset(zero, 0, 4096));
+  hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, x, maxx, 1u, 1.0f);
+  CK(hipMemset(b, 0, 8192 * 4));
+  std::vector<_Float16> hy(maxy), hy0(maxy);
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
+  const char* filt = getenv("CB_SHAPE");   // substring filter on the shape name
   for (auto& s : shapes) {
-    for (int act = 1; act >= 0; --act) {
-      yv7::ConvParams p; memset(&p, 0, sizeof(p));
-      p.x = x; p.y = y; p.w = w; p.bias = (const float*)b; p.zero = zero;
-      p.B = s.B; p.H = s.H; p.W = s.W; p.xc = s.cin; p.xoff = 0; p.cin = s.cin;
-      p.k = s.k; p.s = s.s; p.pad = s.k / 2;
-      p.Ho = (s.H + 2 * p.pad - s.k) / s.s + 1; p.Wo = (s.W + 2 * p.pad - s.k) / s.s + 1;
-      p.yc = s.cout; p.yoff = 0; p.cout = s.cout; p.act = act;
-      p.K = s.k * s.k * s.cin; p.kpad = (p.K + 63) / 64 * 64; p.M = s.B * p.Ho * p.Wo;
-      double flops = 2.0 * p.M * s.cout * p.K;
-      double bytes = 2.0 * ((double)s.B * s.H * s.W * s.cin + (double)p.M * s.cout);
-      printf("%-22s act=%d ", s.name, act);
-      for (int v : variants) {
-        p.variant = v;
-        for (int i = 0; i < 3; ++i) CK(yv7::launch_conv(1, p, false, 0));
-        CK(hipEventRecord(e0, 0));
-        const int it = 10;
-        for (int i = 0; i < it; ++i) CK(yv7::launch_conv(1, p, false, 0));
-        CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
-        float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ms /= it;
-        printf("| v%d %8.1f us %6.0f TF/s %5.2f TB/s ", v, ms * 1e3, flops / ms / 1e9, bytes / ms / 1e9);
+    if (filt && !strstr(s.name, filt)) continue;
+    yv7::ConvParams p; memset(&p, 0, sizeof(p));
+    p.x = x; p.y = y; p.w = w; p.bias = b; p.zero = zero;
+    p.B = s.B; p.H = s.H; p.W = s.W; p.xc = s.cin; p.xoff = 0; p.cin = s.cin;
+    p.k = s.k; p.s = s.s; p.pad = s.k / 2;
+    p.Ho = (s.H + 2 * p.pad - s.k) / s.s + 1; p.Wo = (s.W + 2 * p.pad - s.k) / s.s + 1;
+    p.yc = s.cout; p.yoff = 0; p.cout = s.cout; p.act = 1;
+    p.K = s.k * s.k * s.cin; p.kpad = (p.K + 63) / 64 * 64; p.M = s.B * p.Ho * p.Wo;
+    // weights ~ U(-1,1)/sqrt(K) so outputs stay O(1); padded K columns zero
+    CK(hipMemset(w, 0, maxw * 2));
+    for (int n = 0; n < s.cout; ++n)
+      hipLaunchKernelGGL(fill_rand, dim3(4), dim3(256), 0, 0, w + (size_t)n * p.kpad, (size_t)p.K, 7u + n,
+                         1.0f / sqrtf((float)p.K));
+    const size_t ny = (size_t)p.M * s.cout;
+    double flops = 2.0 * p.M * s.cout * p.K;
+    double bytes = 2.0 * ((double)s.B * s.H * s.W * s.cin + (double)ny);
+    printf("%-22s", s.name);
+    for (int v : variants) {
+      p.variant = v;
+      p.y = v == 0 ? (void*)y0 : (void*)y;
+      for (int i = 0; i < 3; ++i) CK(yv7::launch_conv(1, p, false, 0));
+      CK(hipDeviceSynchronize());
+      CK(hipEventRecord(e0, 0));
+      const int it = 20;
+      for (int i = 0; i < it; ++i) CK(yv7::launch_conv(1, p, false, 0));
+      CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
+      float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ms /= it;
+      double maxd = 0;
+      if (v != 0) {
+        CK(hipMemcpy(hy.data(), y, ny * 2, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(hy0.data(), y0, ny * 2, hipMemcpyDeviceToHost));
+        for (size_t i = 0; i < ny; ++i) maxd = std::max(maxd, (double)fabsf((float)hy[i] - (float)hy0[i]));
       }
-      printf("\n");
+      printf(" | v%d %7.1f us %5.0f TF %4.2f TB/s", v, ms * 1e3, flops / ms / 1e9, bytes / ms / 1e9);
+      if (v != 0) printf(" d=%.3g", maxd);
     }
+    printf("\n");
+    fflush(stdout);
   }
   return 0;
 }

@@ -15,6 +15,7 @@
 //    the tile leaves as full 16-byte NHWC row chunks into the output's channel slice (zero-copy concat);
 //  * XCD-aware bijective block remap: consecutive tiles (all N tiles of an M tile) share an XCD's L2.
 #include <cstdlib>
+#include <type_traits>
 
 #include "yv7_kernels.h"
 
@@ -28,13 +29,48 @@ constexpr int ROWB = 128;  // LDS bytes per tile row
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
-__device__ __forceinline__ float act_fn(float v, int act) {
-  // SiLU with v_exp_f32 / v_rcp_f32 (~1 ulp each): plenty for an fp16 output, ~4x cheaper than the
-  // IEEE expf + division sequence, which otherwise rivals the MFMA time of small-K layers.
-  if (act == 1) return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
-  if (act == 2) return v > 0.0f ? v : v * 0.1f;
-  return v;
+// im2col row setup: base pointer of output pixel (b, ho, wo)'s receptive field and its tap-validity
+// mask (bit r*k+s set when input row r / column s of the window lies inside the image).
+__device__ __forceinline__ void im2col_row(const ConvParams& p, const _Float16* x, int b, int ho, int wo, bool ok,
+                                           const _Float16*& ptr, uint32_t& mask) {
+  const int h0 = ho * p.s - p.pad, w0 = wo * p.s - p.pad;
+  ptr = x + ((ptrdiff_t)(b * p.H + h0) * p.W + w0) * p.xc + p.xoff;
+  uint32_t mk = 0;
+  if (p.k == 3) {
+    const uint32_t rb = (uint32_t)((unsigned)h0 < (unsigned)p.H) | (uint32_t)((unsigned)(h0 + 1) < (unsigned)p.H) << 1 |
+                        (uint32_t)((unsigned)(h0 + 2) < (unsigned)p.H) << 2;
+    const uint32_t cb = (uint32_t)((unsigned)w0 < (unsigned)p.W) | (uint32_t)((unsigned)(w0 + 1) < (unsigned)p.W) << 1 |
+                        (uint32_t)((unsigned)(w0 + 2) < (unsigned)p.W) << 2;
+    mk = ((rb & 1) ? cb : 0u) | ((rb & 2) ? cb << 3 : 0u) | ((rb & 4) ? cb << 6 : 0u);
+  } else {
+    uint32_t rb = 0, cb = 0;
+    for (int r = 0; r < p.k; ++r) rb |= (uint32_t)((unsigned)(h0 + r) < (unsigned)p.H) << r;
+    for (int c = 0; c < p.k; ++c) cb |= (uint32_t)((unsigned)(w0 + c) < (unsigned)p.W) << c;
+    for (int r = 0; r < p.k; ++r)
+      if ((rb >> r) & 1) mk |= cb << (r * p.k);
+  }
+  mask = ok ? mk : 0u;
 }
+
+// Output pixel m -> (b, ho, wo) once, then stepped: rows a thread moves are `step` pixels apart.
+struct PixelWalk {
+  int b, ho, wo;
+  __device__ __forceinline__ PixelWalk(const ConvParams& p, int m) {
+    const int mm = m < p.M ? m : 0;
+    const int hw = p.Ho * p.Wo;
+    b = mm / hw;
+    const int rem = mm - b * hw;
+    ho = rem / p.Wo;
+    wo = rem - ho * p.Wo;
+  }
+  __device__ __forceinline__ void advance(const ConvParams& p, int step) {
+    wo += step;
+    while (wo >= p.Wo) {
+      wo -= p.Wo;
+      if (++ho == p.Ho) { ho = 0; ++b; }
+    }
+  }
+};
 
 template <int BM, int BN, int WM, bool ONE, bool DET>
 __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
@@ -69,26 +105,19 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   // add, one mask test and one 16-byte load per row (im2col address math hoisted out of the loop).
   const _Float16* a_ptr[RA];
   uint32_t a_mask[RA];
+  if (ONE) {
 #pragma unroll
-  for (int j = 0; j < RA; ++j) {
-    const int m = m0 + r0 + 32 * j;
-    const bool ok = m < p.M;
-    const int mm = ok ? m : 0;
-    if (ONE) {
-      a_ptr[j] = x + (size_t)mm * p.xc + p.xoff;
-      a_mask[j] = ok ? 1u : 0u;
-    } else {
-      const int hw = p.Ho * p.Wo;
-      const int b = mm / hw, rem = mm - b * hw;
-      const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
-      const int h0 = ho * p.s - p.pad, w0 = wo * p.s - p.pad;
-      a_ptr[j] = x + ((ptrdiff_t)(b * p.H + h0) * p.W + w0) * p.xc + p.xoff;
-      uint32_t mk = 0;
-      for (int rr = 0; rr < p.k; ++rr)
-        for (int ss = 0; ss < p.k; ++ss)
-          if (ok && (unsigned)(h0 + rr) < (unsigned)p.H && (unsigned)(w0 + ss) < (unsigned)p.W)
-            mk |= 1u << (rr * p.k + ss);
-      a_mask[j] = mk;
+    for (int j = 0; j < RA; ++j) {
+      const int m = m0 + r0 + 32 * j;
+      a_ptr[j] = x + (size_t)(m < p.M ? m : 0) * p.xc + p.xoff;
+      a_mask[j] = m < p.M ? 1u : 0u;
+    }
+  } else {
+    PixelWalk pw(p, m0 + r0);
+#pragma unroll
+    for (int j = 0; j < RA; ++j) {
+      if (j) pw.advance(p, 32);
+      im2col_row(p, x, pw.b, pw.ho, pw.wo, m0 + r0 + 32 * j < p.M, a_ptr[j], a_mask[j]);
     }
   }
   const _Float16* b_ptr[RB];
@@ -152,11 +181,17 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
     }
   };
 
+  // accumulators start at the bias (one VALU add per output element less in the epilogue)
   f4 acc[TN][TM];
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * WTN + j * 16 + g * 4;
+    f4 bv;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) acc[j][i] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = bv;
+  }
 
   gload(0);
   lstore(0);
@@ -207,7 +242,7 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
         const int row = wm * WTM + i * 16 + li;
         f4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e] + ((n0 + col + e < p.cout) ? p.bias[n0 + col + e] : 0.0f);
+        for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e];
         *reinterpret_cast<f4*>(reinterpret_cast<unsigned char*>(Ds) + row * DPITCH + col * 4) = v;
       }
     }
@@ -263,22 +298,22 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   }
 
   unsigned char* Cs = smem;
+  with_act(p.act, [&](auto actc) {
+    constexpr int ACT = decltype(actc)::value;
 #pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = wn * WTN + j * 16 + g * 4;
-    float bias[4];
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WTN + j * 16 + g * 4;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bias[e] = (n0 + col + e < p.cout) ? p.bias[n0 + col + e] : 0.0f;
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WTM + i * 16 + li;
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 v;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = wm * WTM + i * 16 + li;
-      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      h4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (_Float16)act_fn(acc[j][i][e] + bias[e], p.act);
-      *reinterpret_cast<h4*>(Cs + row * CPITCH + col * 2) = v;
+        for (int e = 0; e < 4; ++e) v[e] = (_Float16)act_t<ACT>(acc[j][i][e]);
+        *reinterpret_cast<h4*>(Cs + row * CPITCH + col * 2) = v;
+      }
     }
-  }
+  });
   __syncthreads();
   constexpr int CPR = BN * 2 / 16;
   _Float16* __restrict__ y = reinterpret_cast<_Float16*>(p.y);
@@ -291,23 +326,28 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// v3: LDS-DMA ring.  Operand tiles go global -> LDS with global_load_lds_dwordx4 (no VGPR staging),
-// STAGES-deep ring, counted `s_waitcnt vmcnt` so STAGES-1 K steps stay in flight across the raw
-// s_barrier (never __syncthreads in the loop: its fence would drain the DMA).  Each wave-instruction
-// fills 8 tile rows (1 KiB, lane-linear), so the XOR swizzle is applied on the SOURCE chunk
-// (c = slot ^ (row & 7)) and the ds_read side uses the same swz().  Padding taps and rows beyond
-// M / cout read from a zeroed device page instead of being masked (LDS-DMA cannot zero-fill).
-template <int BM, int BN, int WM, bool ONE, bool DET, int STAGES>
-__global__ __launch_bounds__(NT, 1) void conv_f16_dma_kernel(const ConvParams p) {
-  constexpr int WN = 4 / WM;
+// v4: 8-wave LDS-DMA ring (the main-path kernel for cout >= 64).
+//  * 512 threads = 8 waves (2 per SIMD, so one wave's fragment reads hide under the other's MFMAs),
+//    BM x BN tile, BK = 64, STAGES-deep ring of LDS stages filled by global_load_lds_dwordx4 — no
+//    VGPR staging and no ds_write pass;
+//  * each wave-instruction fills 8 tile rows (1 KiB, lane-linear in LDS), so the XOR swizzle is
+//    applied on the SOURCE chunk (c = slot ^ (row & 7)) and the ds_read side uses the same swz();
+//  * counted `s_waitcnt vmcnt(PER)` keeps the next stage in flight across a raw s_barrier (never
+//    __syncthreads in the loop: its fence would drain the DMA); the stage refilled at step kt is the
+//    one every wave finished reading at step kt-1 (its MFMAs consumed those reads before the barrier);
+//  * padding taps and rows beyond M / cout read a zeroed device page (LDS-DMA cannot zero-fill).
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE>
+__global__ __launch_bounds__(64 * WM * WN, 1) void conv_f16_ring_kernel(const ConvParams p) {
+  constexpr int NW = WM * WN, NTH = 64 * NW;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int RA = BM / 32;            // A wave-instructions per wave per stage (8 rows each)
-  constexpr int RB = (BN + 31) / 32;     // B wave-instructions per wave per stage
-  constexpr int PER = RA + RB;           // vmcnt units per stage per thread
+  constexpr int RA = BM / 8 / NW, RB = BN / 8 / NW;   // wave-instructions per wave per stage
+  static_assert(RA * 8 * NW == BM && RB * 8 * NW == BN, "tile rows must split into 8-row groups per wave");
+  constexpr int PER = RA + RB;
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int CPITCH = BN * 2 + 16;
   constexpr int LDS = (STAGES * STAGE > BM * CPITCH) ? STAGES * STAGE : BM * CPITCH;
+  static_assert(LDS <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
   const int tid = threadIdx.x;
@@ -325,39 +365,31 @@ __global__ __launch_bounds__(NT, 1) void conv_f16_dma_kernel(const ConvParams p)
   const _Float16* __restrict__ w = reinterpret_cast<const _Float16*>(p.w);
   const _Float16* zero = reinterpret_cast<const _Float16*>(p.zero);
 
-  const int lr = lane >> 3;               // row within this wave's 8-row slab (== row & 7)
-  const int c = (lane & 7) ^ lr;          // source chunk this lane fetches (swizzle on the source)
+  const int lr = lane >> 3;            // row within the 8-row group (== row & 7)
+  const int c = (lane & 7) ^ lr;       // source chunk this lane fetches
 
   const _Float16* a_ptr[RA];
   uint32_t a_mask[RA];
+  if (ONE) {
 #pragma unroll
-  for (int j = 0; j < RA; ++j) {
-    const int m = m0 + j * 32 + wave * 8 + lr;
-    const bool ok = m < p.M;
-    const int mm = ok ? m : 0;
-    if (ONE) {
-      a_ptr[j] = x + (size_t)mm * p.xc + p.xoff;
-      a_mask[j] = ok ? 1u : 0u;
-    } else {
-      const int hw = p.Ho * p.Wo;
-      const int b = mm / hw, rem = mm - b * hw;
-      const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
-      const int h0 = ho * p.s - p.pad, w0 = wo * p.s - p.pad;
-      a_ptr[j] = x + ((ptrdiff_t)(b * p.H + h0) * p.W + w0) * p.xc + p.xoff;
-      uint32_t mk = 0;
-      for (int rr = 0; rr < p.k; ++rr)
-        for (int ss = 0; ss < p.k; ++ss)
-          if (ok && (unsigned)(h0 + rr) < (unsigned)p.H && (unsigned)(w0 + ss) < (unsigned)p.W)
-            mk |= 1u << (rr * p.k + ss);
-      a_mask[j] = mk;
+    for (int j = 0; j < RA; ++j) {
+      const int m = m0 + (j * NW + wave) * 8 + lr;
+      a_ptr[j] = x + (size_t)(m < p.M ? m : 0) * p.xc + p.xoff;
+      a_mask[j] = m < p.M ? 1u : 0u;
+    }
+  } else {
+    PixelWalk pw(p, m0 + wave * 8 + lr);
+#pragma unroll
+    for (int j = 0; j < RA; ++j) {
+      if (j) pw.advance(p, NW * 8);
+      im2col_row(p, x, pw.b, pw.ho, pw.wo, m0 + (j * NW + wave) * 8 + lr < p.M, a_ptr[j], a_mask[j]);
     }
   }
   const _Float16* b_ptr[RB];
 #pragma unroll
   for (int j = 0; j < RB; ++j) {
-    const int row = j * 32 + wave * 8 + lr;
-    const bool ok = row < BN && n0 + row < p.cout;
-    b_ptr[j] = ok ? w + (size_t)(n0 + row) * p.kpad + c * 8 : nullptr;
+    const int row = (j * NW + wave) * 8 + lr;
+    b_ptr[j] = n0 + row < p.cout ? w + (size_t)(n0 + row) * p.kpad + c * 8 : nullptr;
   }
 
   const int nk = p.kpad / BKE;
@@ -366,7 +398,6 @@ __global__ __launch_bounds__(NT, 1) void conv_f16_dma_kernel(const ConvParams p)
     while (ci >= p.cin) { ci -= p.cin; ++tap; if (++ss == p.k) { ss = 0; ++rr; } }
   }
 
-  // issue the DMA of K step kt into ring slot `slot`
   auto issue = [&](int kt, int slot) {
     unsigned char* As = smem + slot * STAGE;
     unsigned char* Bs = As + BM * ROWB;
@@ -377,7 +408,7 @@ __global__ __launch_bounds__(NT, 1) void conv_f16_dma_kernel(const ConvParams p)
       for (int j = 0; j < RA; ++j) {
         const _Float16* src = (a_mask[j] && kin) ? a_ptr[j] + k : zero;
         __builtin_amdgcn_global_load_lds((const void*)src,
-                                         (__attribute__((address_space(3))) void*)(As + (j * 32 + wave * 8) * ROWB),
+                                         (__attribute__((address_space(3))) void*)(As + (j * NW + wave) * 8 * ROWB),
                                          16, 0, 0);
       }
     } else {
@@ -387,7 +418,7 @@ __global__ __launch_bounds__(NT, 1) void conv_f16_dma_kernel(const ConvParams p)
       for (int j = 0; j < RA; ++j) {
         const _Float16* src = (a_mask[j] & bit) ? a_ptr[j] + delta : zero;
         __builtin_amdgcn_global_load_lds((const void*)src,
-                                         (__attribute__((address_space(3))) void*)(As + (j * 32 + wave * 8) * ROWB),
+                                         (__attribute__((address_space(3))) void*)(As + (j * NW + wave) * 8 * ROWB),
                                          16, 0, 0);
       }
       ci += BKE;
@@ -397,34 +428,35 @@ __global__ __launch_bounds__(NT, 1) void conv_f16_dma_kernel(const ConvParams p)
     for (int j = 0; j < RB; ++j) {
       const _Float16* src = b_ptr[j] ? b_ptr[j] + kt * BKE : zero;
       __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(Bs + (j * 32 + wave * 8) * ROWB),
+                                       (__attribute__((address_space(3))) void*)(Bs + (j * NW + wave) * 8 * ROWB),
                                        16, 0, 0);
     }
   };
 
+  // accumulators start at the bias (one VALU add per output element less in the epilogue)
   f4 acc[TN][TM];
 #pragma unroll
-  for (int j = 0; j < TN; ++j)
+  for (int j = 0; j < TN; ++j) {
+    const int col = n0 + wn * WTN + j * 16 + g * 4;
+    f4 bv;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) acc[j][i] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = bv;
+  }
 
-  // prologue: STAGES-1 steps in flight
 #pragma unroll
   for (int s0 = 0; s0 < STAGES - 1; ++s0)
     if (s0 < nk) issue(s0, s0);
 
   int slot = 0;
   for (int kt = 0; kt < nk; ++kt) {
-    // retire step kt: the loads issued after it (steps kt+1 .. kt+STAGES-2, if they exist) may stay in flight
-    const int ahead = nk - 1 - kt;  // steps issued after kt so far (capped by STAGES-2)
-    if (STAGES >= 3 && ahead >= 1) {
-      if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
-      else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    // stage kt must have landed; the (at most STAGES-2) stages issued after it may stay in flight
+    const int ahead = nk - 1 - kt;
+    if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (STAGES >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    // refill the slot consumed one iteration ago (every wave has passed the barrier, so its reads are done)
     if (kt + STAGES - 1 < nk) {
       int fs = slot + STAGES - 1;
       if (fs >= STAGES) fs -= STAGES;
@@ -446,76 +478,41 @@ __global__ __launch_bounds__(NT, 1) void conv_f16_dma_kernel(const ConvParams p)
         const int row = wn * WTN + j * 16 + li;
         wb[j] = *reinterpret_cast<const u4*>(Bs + row * ROWB + swz(row, ch) * 16);
       }
+      __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]),
                                                              __builtin_bit_cast(h8, xa[i]), acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
     }
     if (++slot == STAGES) slot = 0;
   }
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
-  if (DET) {
-    const int hw = p.Ho * p.Wo;
+  unsigned char* Cs = smem;
+  with_act(p.act, [&](auto actc) {
+    constexpr int ACT = decltype(actc)::value;
 #pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int m = m0 + wm * WTM + i * 16 + li;
-      if (m >= p.M) continue;
-      const int b = m / hw, rem = m - b * hw;
-      const int gy = rem / p.Wo, gx = rem - gy * p.Wo;
+    for (int j = 0; j < TN; ++j) {
+      const int col = wn * WTN + j * 16 + g * 4;
 #pragma unroll
-      for (int j = 0; j < TN; ++j) {
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WTM + i * 16 + li;
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 v;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int n = n0 + wn * WTN + j * 16 + g * 4 + e;
-          if (n >= p.cout) continue;
-          const int a = n / p.no, o = n - a * p.no;
-          const float v = acc[j][i][e] + p.bias[n];
-          const float sg = 1.0f / (1.0f + expf(-v));
-          float out;
-          if (o < 2) {
-            const float t = sg * 2.0f;
-            const float u = t - 0.5f;
-            out = (u + ((o == 0) ? (float)gx : (float)gy)) * p.stride;
-          } else if (o < 4) {
-            const float t = sg * 2.0f;
-            out = (t * t) * p.anchor[2 * a + (o - 2)];
-          } else {
-            out = sg;
-          }
-          const size_t cell = ((size_t)a * p.Ho + gy) * p.Wo + gx;
-          p.z[(((size_t)b * p.nrows + p.row_off + cell) * p.no) + o] = out;
-          if (p.raw) p.raw[(((size_t)b * p.na * hw) + cell) * p.no + o] = v;
-        }
+        for (int e = 0; e < 4; ++e) v[e] = (_Float16)act_t<ACT>(acc[j][i][e]);
+        *reinterpret_cast<h4*>(Cs + row * CPITCH + col * 2) = v;
       }
     }
-    return;
-  }
-
-  unsigned char* Cs = smem;
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = wn * WTN + j * 16 + g * 4;
-    float bias[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bias[e] = (n0 + col + e < p.cout) ? p.bias[n0 + col + e] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) {
-      const int row = wm * WTM + i * 16 + li;
-      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      h4 v;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[e] = (_Float16)act_fn(acc[j][i][e] + bias[e], p.act);
-      *reinterpret_cast<h4*>(Cs + row * CPITCH + col * 2) = v;
-    }
-  }
+  });
   __syncthreads();
   constexpr int CPR = BN * 2 / 16;
   _Float16* __restrict__ y = reinterpret_cast<_Float16*>(p.y);
-  for (int cc = tid; cc < BM * CPR; cc += NT) {
+  for (int cc = tid; cc < BM * CPR; cc += NTH) {
     const int row = cc / CPR, ch = cc - row * CPR;
     const int m = m0 + row, n = n0 + ch * 8;
     if (m < p.M && n < p.cout)
@@ -523,11 +520,16 @@ __global__ __launch_bounds__(NT, 1) void conv_f16_dma_kernel(const ConvParams p)
   }
 }
 
-template <int BM, int BN, int WM, bool ONE, bool DET, int STAGES>
-hipError_t launch_dma(const ConvParams& p, hipStream_t st) {
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE>
+hipError_t launch_ring(const ConvParams& p, hipStream_t st) {
   const int nM = (p.M + BM - 1) / BM, nN = (p.cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_f16_dma_kernel<BM, BN, WM, ONE, DET, STAGES>), dim3(nM * nN), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, ONE>), dim3(nM * nN), dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+hipError_t launch_ring2(const ConvParams& p, bool one, hipStream_t st) {
+  return one ? launch_ring<BM, BN, WM, WN, STAGES, true>(p, st) : launch_ring<BM, BN, WM, WN, STAGES, false>(p, st);
 }
 
 template <int BM, int BN, int WM, bool ONE, bool DET>
@@ -543,11 +545,24 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   const bool one = p.k == 1 && p.s == 1 && p.pad == 0;
   static const int env_variant = [] { const char* e = getenv("YV7_CONV_F16"); return e ? atoi(e) : 0; }();
   const int variant = p.variant ? p.variant : env_variant;
-  if (variant == 3 && p.zero) {
-    if (det) return launch_dma<128, 128, 2, true, true, 3>(p, st);
-    if (p.cout <= 32) return one ? launch_dma<256, 32, 4, true, false, 3>(p, st) : launch_dma<256, 32, 4, false, false, 3>(p, st);
-    if (p.cout <= 64) return one ? launch_dma<256, 64, 4, true, false, 3>(p, st) : launch_dma<256, 64, 4, false, false, 3>(p, st);
-    return one ? launch_dma<128, 128, 2, true, false, 3>(p, st) : launch_dma<128, 128, 2, false, false, 3>(p, st);
+  if (!det && p.zero && p.cout > 32) {
+    if (variant == 4) {
+      if (p.cout <= 64) return launch_ring2<256, 64, 4, 2, 3>(p, one, st);
+      return launch_ring2<256, 128, 4, 2, 3>(p, one, st);
+    }
+    if (variant == 5) {
+      if (p.cout <= 64) return launch_ring2<512, 64, 8, 1, 2>(p, one, st);
+      if (p.cout <= 128) return launch_ring2<256, 128, 4, 2, 2>(p, one, st);
+      return launch_ring2<256, 256, 2, 4, 2>(p, one, st);
+    }
+    if (variant == 0 && p.cout >= 256) {
+      // wide layers: the 8-wave ring kernels win once their grid still covers the chip
+      // (scripts/convbench.hip, bs 32: 3x3 256->256 @40 112 -> 80 us, 512->1024 @20 208 -> 142 us,
+      // 1x1 512->512 @80 243 -> 216 us); 512->512 @20 has 100 256x256 tiles -> 256x128 (88 vs 102 us)
+      const long mt = (p.M + 255) / 256;
+      if (mt * ((p.cout + 255) / 256) >= 150) return launch_ring2<256, 256, 2, 4, 2>(p, one, st);
+      if (mt * ((p.cout + 127) / 128) >= 150) return launch_ring2<256, 128, 4, 2, 3>(p, one, st);
+    }
   }
   if (det) return launch_t<64, 256, 1, true, true>(p, st);
   if (variant == 2) {  // tall tiles for narrow layers

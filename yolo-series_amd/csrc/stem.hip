@@ -24,12 +24,6 @@ namespace {
 
 constexpr int NT = 256;
 
-__device__ __forceinline__ float act_fast(float v, int act) {
-  if (act == 1) return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
-  if (act == 2) return v > 0.0f ? v : v * 0.1f;
-  return v;
-}
-
 template <typename S, int CA, int CB, int SA, int TBY, int TBX>
 __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   constexpr int TAY = 2 * TBY + 1, TAX = 2 * TBX + 1;      // conv-A pixels feeding the tile
@@ -111,27 +105,38 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
     for (int kk = 0; kk < 8; ++kk) xv[kk] = koff[kk] >= 0 ? patch[base + koff[kk]] : (_Float16)0.f;
     const int ay = ay0 + yl, ax = ax0 + xl;
     const bool inside = m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA;
+    f4 acc[NAT];
 #pragma unroll
     for (int nt = 0; nt < NAT; ++nt) {
-      f4 acc = {0.f, 0.f, 0.f, 0.f};
-      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[nt]), xv, acc, 0, 0, 0);
-      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      h4 o;
+      f4 bv;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int n = nt * 16 + g * 4 + e;
-        o[e] = inside ? (_Float16)act_fast(acc[e] + p.ba[n], p.act_a) : (_Float16)0.f;
-      }
-      if (m < NA) *reinterpret_cast<h4*>(abuf + m * APITCH + (nt * 16 + g * 4) * 2) = o;
+      for (int e = 0; e < 4; ++e) bv[e] = p.ba[nt * 16 + g * 4 + e];
+      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[nt]), xv, bv, 0, 0, 0);
     }
+    with_act(p.act_a, [&](auto actc) {
+      constexpr int ACT = decltype(actc)::value;
+#pragma unroll
+      for (int nt = 0; nt < NAT; ++nt) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) o[e] = inside ? (_Float16)act_t<ACT>(acc[nt][e]) : (_Float16)0.f;
+        if (m < NA) *reinterpret_cast<h4*>(abuf + m * APITCH + (nt * 16 + g * 4) * 2) = o;
+      }
+    });
   }
   __syncthreads();
 
   // 3. conv B: wave w owns output channels [16w, 16w+16) for every pixel of the tile; its 9 taps of
   //    weight fragments were loaded at kernel entry (wfr), so no global load sits in this loop.
   f4 acc[MB];
+  {
+    f4 bv;
 #pragma unroll
-  for (int i = 0; i < MB; ++i) acc[i] = f4{0.f, 0.f, 0.f, 0.f};
+    for (int e = 0; e < 4; ++e) bv[e] = p.bb[wave * 16 + g * 4 + e];
+#pragma unroll
+    for (int i = 0; i < MB; ++i) acc[i] = bv;
+  }
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
     const int r = tap / 3, s = tap - r * 3;
@@ -150,18 +155,18 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   // 4. epilogue via LDS: lane holds 4 consecutive channels of one conv-B pixel
   {
     const int col = wave * 16 + g * 4;
-    float bias[4];
+    with_act(p.act_b, [&](auto actc) {
+      constexpr int ACT = decltype(actc)::value;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bias[e] = p.bb[col + e];
+      for (int i = 0; i < MB; ++i) {
+        const int mb = i * 16 + li;
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 o;
 #pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const int mb = i * 16 + li;
-      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      h4 o;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) o[e] = (_Float16)act_fast(acc[i][e] + bias[e], p.act_b);
-      *reinterpret_cast<h4*>(smem + mb * CPITCH + col * 2) = o;
-    }
+        for (int e = 0; e < 4; ++e) o[e] = (_Float16)act_t<ACT>(acc[i][e]);
+        *reinterpret_cast<h4*>(smem + mb * CPITCH + col * 2) = o;
+      }
+    });
   }
   __syncthreads();
   constexpr int CPR = CB * 2 / 16;

@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace yv7 {
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
@@ -13,6 +15,24 @@ typedef uint32_t u4 __attribute__((ext_vector_type(4)));
 template <typename T> struct Vec;
 template <> struct Vec<_Float16> { static constexpr int N = 8; };
 template <> struct Vec<float> { static constexpr int N = 4; };
+
+template <int ACT>
+__device__ __forceinline__ float act_t(float v) {
+  // SiLU with v_exp_f32 / v_rcp_f32 (~1 ulp each): plenty for an fp16 output, ~4x cheaper than the
+  // IEEE expf + division sequence, which otherwise rivals the MFMA time of small-K layers.
+  if constexpr (ACT == 1) return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
+  if constexpr (ACT == 2) return v > 0.0f ? v : v * 0.1f;
+  return v;
+}
+
+// Calls f(std::integral_constant<int, ACT>) with the layer's activation as a compile-time constant, so
+// an epilogue is straight-line code (a runtime switch per element costs more than the SiLU itself).
+template <typename F>
+__device__ __forceinline__ void with_act(int act, F&& f) {
+  if (act == 1) f(std::integral_constant<int, 1>{});
+  else if (act == 2) f(std::integral_constant<int, 2>{});
+  else f(std::integral_constant<int, 0>{});
+}
 
 // Kernel parameters of one conv launch (also the fused Detect head).
 struct ConvParams {

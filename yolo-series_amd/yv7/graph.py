@@ -237,13 +237,13 @@ def compile_model(model, dtype: int) -> Graph:
         return loc[i]
 
     def conv_op(src, dst, w, b, k, s, pad, act):
+        # weights are packed after the sibling-merge pass (_merge_siblings), so they ride along unpacked
         (ts, so, cs), (td, do) = src, dst
         cin_pad = _rup(cs, V)
         if cin_pad != cs and g.tensors[ts][0] < so + cin_pad:
             raise ValueError('channel padding would read outside the source tensor')
-        w_off, b_off = _pack_conv(g, w, b, cin_pad)
         g.ops.append(dict(kind=L.OP_CONV, src=ts, src_coff=so, cin=cin_pad, dst=td, dst_coff=do, cout=w.shape[0],
-                          k=k, s=s, pad=pad, act=act, w_off=w_off, b_off=b_off))
+                          k=k, s=s, pad=pad, act=act, _w=w, _b=b))
 
     for m in layers:
         i = m.i
@@ -329,5 +329,73 @@ def compile_model(model, dtype: int) -> Graph:
                 w_off, b_off = _pack_conv(g, w, b, _rup(cs, V))
                 g.ops.append(dict(kind=L.OP_DETECT, src=ts, src_coff=so, cin=_rup(cs, V), dst=-1, cout=w.shape[0],
                                   k=1, s=1, pad=0, level=lvl, w_off=w_off, b_off=b_off))
+    if os.environ.get('YV7_NO_MERGE') != '1':
+        _merge_siblings(g)
+    for o in g.ops:
+        if '_w' in o:
+            o['w_off'], o['b_off'] = _pack_conv(g, o.pop('_w'), o.pop('_b'), o['cin'])
     g.layer_tensor = {i: (loc[i][0], loc[i][1], ch[i]) for i in loc}
     return g
+
+
+def _writes(o):
+    """(tensor, first channel, channels) an op writes, or None (DETECT writes z)."""
+    if o['kind'] == L.OP_DETECT:
+        return None
+    if o['kind'] == L.OP_STEM:
+        return o['dst'], o['dst_coff'], o['cout2']
+    return o['dst'], o['dst_coff'], o['cout']
+
+
+def _merge_siblings(g: Graph):
+    """Fold pairs of CONV ops that read the same input slice with the same geometry and activation and
+    write adjacent channel slices of one tensor into a single GEMM with N = cout_a + cout_b.
+
+    In every ELAN block the two 1x1 entry convs (e.g. yolov7.yaml:20-21 `[-1, 1, Conv, [64, 1, 1]]`,
+    `[-2, 1, Conv, [64, 1, 1]]`) both read the previous layer and land side by side in the block's
+    concat (`[[-1, -3, -5, -6], 1, Concat, [1]]` puts -5 and -6 next to each other): one launch then
+    reads the input once and runs a GEMM twice as wide.  Output bytes are unchanged."""
+    key = ('src', 'src_coff', 'cin', 'k', 's', 'pad', 'act', 'dst')
+    i = 0
+    while i < len(g.ops):
+        a = g.ops[i]
+        if a['kind'] != L.OP_CONV or '_w' not in a:
+            i += 1
+            continue
+        for j in range(i + 1, len(g.ops)):
+            b = g.ops[j]
+            w = _writes(b)
+            if b['kind'] == L.OP_CONV and '_w' in b and all(a[k] == b[k] for k in key):
+                if b['dst_coff'] == a['dst_coff'] + a['cout']:
+                    lo, hi = a, b
+                elif a['dst_coff'] == b['dst_coff'] + b['cout']:
+                    lo, hi = b, a
+                else:
+                    lo = None
+                if lo is not None:
+                    # b moves up to a's position: nothing in between may write b's input or read/write b's output
+                    between = g.ops[i + 1:j]
+                    ok = True
+                    for o in between:
+                        wo = _writes(o)
+                        if wo and wo[0] == b['src'] and wo[1] < b['src_coff'] + b['cin'] and b['src_coff'] < wo[1] + wo[2]:
+                            ok = False
+                        if wo and wo[0] == b['dst'] and wo[1] < b['dst_coff'] + b['cout'] and b['dst_coff'] < wo[1] + wo[2]:
+                            ok = False
+                        rs = o.get('src', -1)
+                        if rs == b['dst'] and o.get('src_coff', 0) < b['dst_coff'] + b['cout'] and \
+                                b['dst_coff'] < o.get('src_coff', 0) + max(o.get('cin', 0), o.get('cout', 0)):
+                            ok = False
+                    if ok:
+                        m = dict(a)
+                        m['dst_coff'] = lo['dst_coff']
+                        m['cout'] = a['cout'] + b['cout']
+                        m['_w'] = torch.cat([lo['_w'], hi['_w']], 0)
+                        m['_b'] = torch.cat([lo['_b'], hi['_b']], 0)
+                        m['merged'] = (lo['cout'], hi['cout'])
+                        g.ops[i] = m
+                        del g.ops[j]
+                        break
+            if w and w[0] == a['src'] and w[1] < a['src_coff'] + a['cin'] and a['src_coff'] < w[1] + w[2]:
+                break  # a's input is overwritten from here on
+        i += 1

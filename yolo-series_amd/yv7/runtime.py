@@ -27,7 +27,7 @@ class Plan:
         for o in graph.ops:
             d = dict(kind=0, src=0, src_coff=0, cin=0, dst=0, dst_coff=0, cout=0, k=1, s=1, pad=0, act=0, level=0,
                      w_off=0, b_off=0, cout2=0, act2=0, w2_off=0, b2_off=0)
-            d.update(o)
+            d.update({k: v for k, v in o.items() if k in d})
             ops.append(L.OpDesc(**d))
         self._ops = (L.OpDesc * len(ops))(*ops)
         self._stride = (ctypes.c_float * graph.nl)(*graph.stride)
