@@ -64,3 +64,40 @@ def test_weight_packing_round_trip():
     assert torch.equal(unpacked, w)
     assert torch.equal(blob[op['b_off']:op['b_off'] + cout * 4].view(torch.float32), b)
     assert torch.all(W[:, k * k * cin:] == 0) and torch.all(W[cout:] == 0)
+
+
+@pytest.mark.parametrize('name', ['yolov7-tiny', 'yolov7', 'yolov7-w6'])
+def test_plan_semantics_vs_oracle(name):
+    """The compiled fp32 plan, executed op by op on the CPU (tests/plan_interp.py), reproduces the
+    oracle's z: concat placement, pool cascade, sibling merging and detect rows are all exercised."""
+    import plan_interp
+    from helpers import frames, oracle_net
+    from oracle import yolo_ref
+    m = fresh_model(name)
+    g = compile_model(m, L.DT_F32)
+    assert any('merged' in o for o in g.ops)
+    s = 128 if 'w6' in name else 64
+    x = frames(1, s, s)
+    net, fused = oracle_net(name)
+    with torch.no_grad():
+        want = yolo_ref.forward(net, fused, x)[0]
+        got = plan_interp.run(g, x)
+    assert got.shape == want.shape
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-3)
+
+
+def test_sibling_merge(monkeypatch):
+    """ELAN entry pairs fold into one GEMM whose packed weights are the two convs' rows back to back,
+    written where the pair's concat slices sit; the f16 plan (fused stem) keeps its semantics."""
+    import plan_interp
+    from helpers import frames
+    m = fresh_model('yolov7')
+    g = compile_model(m, L.DT_F16)
+    merged = [o for o in g.ops if 'merged' in o]
+    assert len(merged) == 8                          # 4 backbone ELAN + 4 head ELAN-H blocks
+    monkeypatch.setenv('YV7_NO_MERGE', '1')
+    g0 = compile_model(m, L.DT_F16)
+    assert len(g0.ops) == len(g.ops) + 8 and not any('merged' in o for o in g0.ops)
+    x = frames(1, 64, 64)
+    with torch.no_grad():
+        torch.testing.assert_close(plan_interp.run(g, x), plan_interp.run(g0, x), rtol=0, atol=0)

@@ -337,7 +337,7 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
 //    one every wave finished reading at step kt-1 (its MFMAs consumed those reads before the barrier);
 //  * padding taps and rows beyond M / cout read a zeroed device page (LDS-DMA cannot zero-fill).
 template <int BM, int BN, int WM, int WN, int STAGES, bool ONE>
-__global__ __launch_bounds__(64 * WM * WN, 1) void conv_f16_ring_kernel(const ConvParams p) {
+__global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 1024) ? 2 : 1) void conv_f16_ring_kernel(const ConvParams p) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
@@ -554,6 +554,14 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
       if (p.cout <= 64) return launch_ring2<512, 64, 8, 1, 2>(p, one, st);
       if (p.cout <= 128) return launch_ring2<256, 128, 4, 2, 2>(p, one, st);
       return launch_ring2<256, 256, 2, 4, 2>(p, one, st);
+    }
+    if (variant == 6) {
+      if (p.cout <= 64) return launch_ring2<128, 64, 2, 2, 3>(p, one, st);
+      return launch_ring2<128, 128, 2, 2, 2>(p, one, st);
+    }
+    if (variant == 7) {
+      if (p.cout <= 64) return launch_ring2<128, 64, 2, 2, 4>(p, one, st);
+      return launch_ring2<128, 128, 2, 2, 3>(p, one, st);
     }
     if (variant == 0 && p.cout >= 256) {
       // wide layers: the 8-wave ring kernels win once their grid still covers the chip
