@@ -29,7 +29,13 @@
 extern "C" {
 #endif
 
-#define YV7_ABI_VERSION 1
+#define YV7_ABI_VERSION 2
+
+/* Activation tensors in the forward workspace are NHWC with a YV7_BORDER-pixel zero frame around
+ * every image: [B][h + 2*YV7_BORDER][w + 2*YV7_BORDER][C].  Kernels write only interiors; the frame
+ * serves every 3x3 / pad-1 window's out-of-image taps.  yv7_forward clears the workspace the first
+ * time it sees it (pointer and size), so between calls the workspace must belong to that plan. */
+#define YV7_BORDER 1
 
 typedef enum {
   YV7_OK = 0,
@@ -113,8 +119,9 @@ int yv7_forward(yv7_plan* plan, const void* x, int x_dtype, int B, int H, int W,
 int yv7_profile_enable(yv7_plan* plan, int max_forwards);
 int yv7_profile_read(yv7_plan* plan, int* n_forwards, float* op_ms);
 
-/* Byte offset of activation tensor `tensor_id` inside the forward workspace and its NHWC dims
- * [B, H', W', channels] — lets a caller read any intermediate layer for per-layer parity checks. */
+/* Byte offset of activation tensor `tensor_id` inside the forward workspace and its bordered NHWC dims
+ * (B, h + 2*YV7_BORDER, w + 2*YV7_BORDER, C); the image interior starts at [YV7_BORDER][YV7_BORDER].
+ * Lets a caller read any intermediate layer for per-layer parity checks. */
 int yv7_tensor_info(const yv7_plan* plan, int tensor_id, int B, int H, int W, int64_t* offset,
                     int64_t* dims4);
 

@@ -44,8 +44,8 @@ int main(int argc, char** argv) {
   if (variants.empty()) variants = {0, 4, 5};
   size_t maxx = 0, maxy = 0, maxw = 0;
   for (auto& s : shapes) {
-    maxx = std::max(maxx, (size_t)s.B * s.H * s.W * s.cin);
-    maxy = std::max(maxy, (size_t)s.B * (s.H / s.s) * (s.W / s.s) * s.cout);
+    maxx = std::max(maxx, yv7::bordered_pixels(s.B, s.H, s.W) * s.cin);
+    maxy = std::max(maxy, yv7::bordered_pixels(s.B, s.H / s.s, s.W / s.s) * s.cout);
     maxw = std::max(maxw, (size_t)((s.cout + 31) / 32 * 32) * ((s.k * s.k * s.cin + 63) / 64 * 64));
   }
   _Float16 *x, *y, *y0, *w;
@@ -53,6 +53,7 @@ int main(int argc, char** argv) {
   void* zero;
   CK(hipMalloc(&x, maxx * 2)); CK(hipMalloc(&y, maxy * 2)); CK(hipMalloc(&y0, maxy * 2)); CK(hipMalloc(&w, maxw * 2));
   CK(hipMalloc(&b, 8192 * 4)); CK(hipMalloc(&zero, 4096)); CK(hipMemset(zero, 0, 4096));
+  CK(hipMemset(y, 0, maxy * 2)); CK(hipMemset(y0, 0, maxy * 2));
   hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, x, maxx, 1u, 1.0f);
   CK(hipMemset(b, 0, 8192 * 4));
   std::vector<_Float16> hy(maxy), hy0(maxy);
@@ -67,12 +68,14 @@ int main(int argc, char** argv) {
     p.Ho = (s.H + 2 * p.pad - s.k) / s.s + 1; p.Wo = (s.W + 2 * p.pad - s.k) / s.s + 1;
     p.yc = s.cout; p.yoff = 0; p.cout = s.cout; p.act = 1;
     p.K = s.k * s.k * s.cin; p.kpad = (p.K + 63) / 64 * 64; p.M = s.B * p.Ho * p.Wo;
+    p.xbytes = (uint32_t)(yv7::bordered_pixels(s.B, s.H, s.W) * s.cin * 2);
+    p.wbytes = (uint32_t)((size_t)(s.cout + 31) / 32 * 32 * p.kpad * 2);
     // weights ~ U(-1,1)/sqrt(K) so outputs stay O(1); padded K columns zero
     CK(hipMemset(w, 0, maxw * 2));
     for (int n = 0; n < s.cout; ++n)
       hipLaunchKernelGGL(fill_rand, dim3(4), dim3(256), 0, 0, w + (size_t)n * p.kpad, (size_t)p.K, 7u + n,
                          1.0f / sqrtf((float)p.K));
-    const size_t ny = (size_t)p.M * s.cout;
+    const size_t ny = yv7::bordered_pixels(s.B, p.Ho, p.Wo) * s.cout;
     double flops = 2.0 * p.M * s.cout * p.K;
     double bytes = 2.0 * ((double)s.B * s.H * s.W * s.cin + (double)ny);
     printf("%-22s", s.name);

@@ -80,27 +80,21 @@ __global__ __launch_bounds__(NT) void conv_kernel(const ConvParams p) {
   const T* __restrict__ x = reinterpret_cast<const T*>(p.x);
   const T* __restrict__ w = reinterpret_cast<const T*>(p.w);
 
-  // ---- per-thread A-row precompute
+  // ---- per-thread A-row precompute (bordered input: see BORDER in yv7_kernels.h)
   const int cA = tid & 3;                 // chunk column this thread loads (A and B)
-  int a_pix[NA];                          // pixel index base (b*H*W) for general conv, or row m for 1x1
-  int a_h[NA], a_w[NA];
+  int a_b[NA], a_h[NA], a_w[NA];
   bool a_ok[NA];
 #pragma unroll
   for (int j = 0; j < NA; ++j) {
     const int m = m0 + (tid >> 2) + 64 * j;
     a_ok[j] = m < p.M;
     const int mm = a_ok[j] ? m : 0;
-    if (ONE) {
-      a_pix[j] = mm;
-      a_h[j] = a_w[j] = 0;
-    } else {
-      const int hw = p.Ho * p.Wo;
-      const int b = mm / hw, rem = mm - b * hw;
-      const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
-      a_pix[j] = b * p.H * p.W;
-      a_h[j] = ho * p.s - p.pad;
-      a_w[j] = wo * p.s - p.pad;
-    }
+    const int hw = p.Ho * p.Wo;
+    const int b = mm / hw, rem = mm - b * hw;
+    const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+    a_b[j] = b;
+    a_h[j] = ho * p.s - p.pad;
+    a_w[j] = wo * p.s - p.pad;
   }
 
   u4 ra[NA], rb[NB];
@@ -108,25 +102,16 @@ __global__ __launch_bounds__(NT) void conv_kernel(const ConvParams p) {
 
   auto gload = [&](int kt) {
     const int k = kt * BKE + cA * V;
-    if (ONE) {
+    int tap = 0, ci = k;
+    if (!ONE && k < p.K) { tap = k / p.cin; ci = k - tap * p.cin; }
+    const int rr = ONE ? 0 : tap / p.k, ss = ONE ? 0 : tap - rr * p.k;
 #pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        u4 v = {0u, 0u, 0u, 0u};
-        if (a_ok[j] && k < p.K) v = *reinterpret_cast<const u4*>(x + (size_t)a_pix[j] * p.xc + p.xoff + k);
-        ra[j] = v;
-      }
-    } else {
-      int tap = 0, ci = k;
-      if (k < p.K) { tap = k / p.cin; ci = k - tap * p.cin; }
-      const int rr = tap / p.k, ss = tap - rr * p.k;
-#pragma unroll
-      for (int j = 0; j < NA; ++j) {
-        u4 v = {0u, 0u, 0u, 0u};
-        const int hi = a_h[j] + rr, wi = a_w[j] + ss;
-        if (a_ok[j] && k < p.K && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
-          v = *reinterpret_cast<const u4*>(x + ((size_t)a_pix[j] + (size_t)hi * p.W + wi) * p.xc + p.xoff + ci);
-        ra[j] = v;
-      }
+    for (int j = 0; j < NA; ++j) {
+      u4 v = {0u, 0u, 0u, 0u};
+      const int hi = a_h[j] + rr, wi = a_w[j] + ss;
+      if (a_ok[j] && k < p.K && (unsigned)hi < (unsigned)p.H && (unsigned)wi < (unsigned)p.W)
+        v = *reinterpret_cast<const u4*>(x + pix_index(a_b[j], hi, wi, p.H, p.W) * p.xc + p.xoff + ci);
+      ra[j] = v;
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
@@ -241,12 +226,16 @@ __global__ __launch_bounds__(NT) void conv_kernel(const ConvParams p) {
   __syncthreads();
   constexpr int CPR = BN * (int)sizeof(T) / 16;   // chunks per row
   T* __restrict__ y = reinterpret_cast<T*>(p.y);
+  const int hw = p.Ho * p.Wo;
   for (int c = tid; c < BM * CPR; c += NT) {
     const int row = c / CPR, ch = c - row * CPR;
     const int m = m0 + row, n = n0 + ch * V;
-    if (m < p.M && n < p.cout)
-      *reinterpret_cast<u4*>(y + (size_t)m * p.yc + p.yoff + n) =
+    if (m < p.M && n < p.cout) {
+      const int b = m / hw, rem = m - b * hw;
+      const int ho = rem / p.Wo, wo = rem - ho * p.Wo;
+      *reinterpret_cast<u4*>(y + pix_index(b, ho, wo, p.Ho, p.Wo) * p.yc + p.yoff + n) =
           *reinterpret_cast<const u4*>(Cs + row * CPITCH + ch * 16);
+    }
   }
 }
 

@@ -1,19 +1,25 @@
-// fp16 implicit-GEMM convolution for gfx950 (the bench / serving path), NHWC activations, KRSC weights.
+// fp16 implicit-GEMM convolution for gfx950 (the bench / serving path), bordered NHWC activations,
+// KRSC weights.
 //
 // Replaces ATen conv2d + BN-folded bias + SiLU/LeakyReLU (Conv.fuseforward models/common.py:110-111,
 // RepConv deploy common.py:498-500) and the Detect head conv + decode (models/yolo.py:46-57).
 //
-// GEMM view: M = B*Ho*Wo pixels, N = cout, K = k*k*cin ordered (r, s, ci).  A 256-thread block
-// (4 waves, WM x WN) owns a BM x BN tile; every wave a (BM/WM) x (BN/WN) sub-tile of 16x16 MFMA tiles.
+// GEMM view: M = B*Ho*Wo pixels, N = cout, K = k*k*cin ordered (r, s, ci).
 //  * K step 64 (128 bytes per tile row), two v_mfma_f32_16x16x32_f16 sub-steps per tile per step;
+//  * operands come in through raw buffer loads: each tile row (an output pixel's receptive-field
+//    origin in the bordered input, or a weight row) is a per-lane byte offset computed once, the K
+//    step's tap / channel position is a scalar offset (cin % 64 == 0: a K step never straddles two
+//    taps), and the zero frame around every image replaces the padding tests — the K loop spends no
+//    vector instructions on addressing.  Rows past M / cout land beyond the buffer range: zeros;
 //  * LDS rows of 8 x 16-byte chunks, chunk index XOR-swizzled with (row & 7) so the 16-lane groups
-//    of ds_read_b128 hit distinct 16-byte slots; double-buffered, one barrier per K step;
-//  * next step's global loads are issued into registers before this step's MFMAs and written to
-//    the other LDS buffer after them (issue-early / write-late);
+//    of ds_read_b128 hit distinct 16-byte slots;
 //  * operands swapped (weights as the MFMA A operand) so each lane's accumulator holds 4
 //    consecutive output channels of one pixel: the epilogue packs them into 8-byte LDS writes, and
 //    the tile leaves as full 16-byte NHWC row chunks into the output's channel slice (zero-copy concat);
+//  * accumulators start at the bias; the activation is a compile-time constant in the epilogue;
 //  * XCD-aware bijective block remap: consecutive tiles (all N tiles of an M tile) share an XCD's L2.
+// Two main loops: the 4-wave register-staged tile kernel (2-3 blocks per CU, any width) and the
+// 8-wave LDS-DMA ring for wide layers.
 #include <cstdlib>
 #include <type_traits>
 
@@ -26,40 +32,23 @@ namespace {
 constexpr int NT = 256;
 constexpr int BKE = 64;    // K elements per step
 constexpr int ROWB = 128;  // LDS bytes per tile row
+constexpr uint32_t OOB = 0x80000000u;  // a buffer offset past every tensor: the load returns zeros
 
 __device__ __forceinline__ int swz(int row, int chunk) { return chunk ^ (row & 7); }
 
-// im2col row setup: base pointer of output pixel (b, ho, wo)'s receptive field and its tap-validity
-// mask (bit r*k+s set when input row r / column s of the window lies inside the image).
-__device__ __forceinline__ void im2col_row(const ConvParams& p, const _Float16* x, int b, int ho, int wo, bool ok,
-                                           const _Float16*& ptr, uint32_t& mask) {
-  const int h0 = ho * p.s - p.pad, w0 = wo * p.s - p.pad;
-  ptr = x + ((ptrdiff_t)(b * p.H + h0) * p.W + w0) * p.xc + p.xoff;
-  uint32_t mk = 0;
-  if (p.k == 3) {
-    const uint32_t rb = (uint32_t)((unsigned)h0 < (unsigned)p.H) | (uint32_t)((unsigned)(h0 + 1) < (unsigned)p.H) << 1 |
-                        (uint32_t)((unsigned)(h0 + 2) < (unsigned)p.H) << 2;
-    const uint32_t cb = (uint32_t)((unsigned)w0 < (unsigned)p.W) | (uint32_t)((unsigned)(w0 + 1) < (unsigned)p.W) << 1 |
-                        (uint32_t)((unsigned)(w0 + 2) < (unsigned)p.W) << 2;
-    mk = ((rb & 1) ? cb : 0u) | ((rb & 2) ? cb << 3 : 0u) | ((rb & 4) ? cb << 6 : 0u);
-  } else {
-    uint32_t rb = 0, cb = 0;
-    for (int r = 0; r < p.k; ++r) rb |= (uint32_t)((unsigned)(h0 + r) < (unsigned)p.H) << r;
-    for (int c = 0; c < p.k; ++c) cb |= (uint32_t)((unsigned)(w0 + c) < (unsigned)p.W) << c;
-    for (int r = 0; r < p.k; ++r)
-      if ((rb >> r) & 1) mk |= cb << (r * p.k);
-  }
-  mask = ok ? mk : 0u;
+// 16 bytes per lane from a buffer straight into LDS (lane-linear at the wave-uniform `lds` base)
+__device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t vo, uint32_t so) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, vo, so, 0, 0);
 }
 
 // Output pixel m -> (b, ho, wo) once, then stepped: rows a thread moves are `step` pixels apart.
+// Rows past M walk into image B, whose offsets lie beyond the input buffer (zeros).
 struct PixelWalk {
   int b, ho, wo;
   __device__ __forceinline__ PixelWalk(const ConvParams& p, int m) {
-    const int mm = m < p.M ? m : 0;
     const int hw = p.Ho * p.Wo;
-    b = mm / hw;
-    const int rem = mm - b * hw;
+    b = m / hw;
+    const int rem = m - b * hw;
     ho = rem / p.Wo;
     wo = rem - ho * p.Wo;
   }
@@ -72,7 +61,73 @@ struct PixelWalk {
   }
 };
 
-template <int BM, int BN, int WM, bool ONE, bool DET>
+// Byte offset in the bordered input of output pixel (b, ho, wo)'s receptive-field origin (tap 0,0),
+// channel xoff + 8 * chunk.
+__device__ __forceinline__ uint32_t a_origin(const ConvParams& p, int b, int ho, int wo, int chunk) {
+  return (uint32_t)((pix_index(b, ho * p.s - p.pad, wo * p.s - p.pad, p.H, p.W) * p.xc + p.xoff + chunk * 8) * 2);
+}
+
+// The K-step cursor: tap (rr, ss) and channel ci of a K position, advanced 64 at a time.
+struct KCursor {
+  int ci, rr, ss, tap;
+  __device__ __forceinline__ void init(const ConvParams& p, int k) {
+    ci = k; rr = ss = tap = 0;
+    while (ci >= p.cin) { ci -= p.cin; ++tap; if (++ss == p.k) { ss = 0; ++rr; } }
+  }
+  __device__ __forceinline__ void advance(const ConvParams& p) {
+    ci += BKE;
+    while (ci >= p.cin) { ci -= p.cin; ++tap; if (++ss == p.k) { ss = 0; ++rr; } }
+  }
+  // byte offset of (rr, ss, ci) relative to the receptive-field origin
+  __device__ __forceinline__ uint32_t offset(const ConvParams& p) const {
+    return (uint32_t)(((rr * (p.W + 2 * BORDER) + ss) * p.xc + ci) * 2);
+  }
+};
+
+// A-operand source of one K step for RA rows: uniform case (1x1, or cin % 64 == 0) = per-row offset
+// + scalar step offset; otherwise per-lane tap tracking (cin of 8..56: tiny's narrow layers).
+template <bool ONE, int RA>
+struct AWalk {
+  uint32_t off[RA];   // row origin + this lane's chunk
+  KCursor su;         // uniform cursor (k = kt*64)
+  KCursor ln;         // per-lane cursor (k = kt*64 + chunk*8), non-uniform case only
+  bool uni;
+  int c16;
+  __device__ __forceinline__ void init(const ConvParams& p, int chunk) {
+    uni = ONE || (p.cin & 63) == 0;
+    c16 = chunk * 16;
+    su.init(p, 0);
+    if (!uni) ln.init(p, chunk * 8);
+  }
+  // voffset / soffset of row j for step kt (call step() once per K step, in order)
+  template <typename F>
+  __device__ __forceinline__ void step(const ConvParams& p, int kt, F&& load) {
+    if (ONE) {
+      const uint32_t so = (uint32_t)kt * BKE * 2;
+      if ((kt + 1) * BKE <= p.K) {
+#pragma unroll
+        for (int j = 0; j < RA; ++j) load(j, off[j], so);
+      } else {   // ragged last step (cin % 64 != 0): lanes past K read zeros
+        const bool kin = kt * BKE + c16 / 2 < p.K;
+#pragma unroll
+        for (int j = 0; j < RA; ++j) load(j, kin ? off[j] : OOB, so);
+      }
+    } else if (uni) {
+      const uint32_t so = su.offset(p);
+      su.advance(p);
+#pragma unroll
+      for (int j = 0; j < RA; ++j) load(j, off[j], so);
+    } else {
+      const bool kin = kt * BKE + c16 / 2 < p.K;
+      const uint32_t d = ln.offset(p) - (uint32_t)c16;
+      ln.advance(p);
+#pragma unroll
+      for (int j = 0; j < RA; ++j) load(j, kin ? off[j] + d : OOB, 0u);
+    }
+  }
+};
+
+template <int BM, int BN, int WM, bool ONE, bool DET, int PF = 1>
 __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   constexpr int WN = 4 / WM;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -81,7 +136,8 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   constexpr int RB = (BN + 31) / 32;
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int CPITCH = BN * 2 + 16;
-  constexpr int LDS = (2 * STAGE > BM * CPITCH) ? 2 * STAGE : BM * CPITCH;
+  constexpr int EPI = BM * CPITCH + BM * 4;   // staged C tile + output row table
+  constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
   const int tid = threadIdx.x;
@@ -95,78 +151,36 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   const int nN = (p.cout + BN - 1) / BN;
   const int m0 = (wgid / nN) * BM, n0 = (wgid % nN) * BN;
 
-  const _Float16* __restrict__ x = reinterpret_cast<const _Float16*>(p.x);
-  const _Float16* __restrict__ w = reinterpret_cast<const _Float16*>(p.w);
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto wr = make_rsrc(p.w, p.wbytes);
 
   const int c = tid & 7;     // 16-byte chunk column this thread moves
-  const int r0 = tid >> 3;   // first row this thread moves
+  const int r0 = tid >> 3;   // first row this thread moves (then every 32nd)
 
-  // Per-row source pointers and tap-validity masks, computed once: a K step then costs one pointer
-  // add, one mask test and one 16-byte load per row (im2col address math hoisted out of the loop).
-  const _Float16* a_ptr[RA];
-  uint32_t a_mask[RA];
-  if (ONE) {
-#pragma unroll
-    for (int j = 0; j < RA; ++j) {
-      const int m = m0 + r0 + 32 * j;
-      a_ptr[j] = x + (size_t)(m < p.M ? m : 0) * p.xc + p.xoff;
-      a_mask[j] = m < p.M ? 1u : 0u;
-    }
-  } else {
+  AWalk<ONE, RA> aw;
+  aw.init(p, c);
+  {
     PixelWalk pw(p, m0 + r0);
 #pragma unroll
     for (int j = 0; j < RA; ++j) {
       if (j) pw.advance(p, 32);
-      im2col_row(p, x, pw.b, pw.ho, pw.wo, m0 + r0 + 32 * j < p.M, a_ptr[j], a_mask[j]);
+      aw.off[j] = a_origin(p, pw.b, pw.ho, pw.wo, c);
     }
   }
-  const _Float16* b_ptr[RB];
-  bool b_ok[RB];
+  uint32_t b_off[RB];   // weight rows past cout_pad32 fall beyond the weight buffer (zeros)
 #pragma unroll
-  for (int j = 0; j < RB; ++j) {
-    const int row = r0 + 32 * j;
-    b_ok[j] = row < BN && n0 + row < p.cout;
-    b_ptr[j] = w + (size_t)(b_ok[j] ? n0 + row : 0) * p.kpad + c * 8;
-  }
+  for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)(((n0 + r0 + 32 * j) * p.kpad + c * 8) * 2);
 
-  u4 ra[RA], rb[RB];
   const int nk = p.kpad / BKE;
-  // K position of this thread's chunk: k = kt*64 + c*8 = tap*cin + ci, tap = rr*k + ss (incremental)
-  int ci = c * 8, tap = 0, rr = 0, ss = 0;
-  if (!ONE) {
-    while (ci >= p.cin) { ci -= p.cin; ++tap; if (++ss == p.k) { ss = 0; ++rr; } }
-  }
-
-  auto gload = [&](int kt) {
-    const int k = kt * BKE + c * 8;
-    const bool kin = k < p.K;
-    if (ONE) {
+  auto gload = [&](int kt, u4 (&ra)[RA], u4 (&rb)[RB]) {
+    aw.step(p, kt, [&](int j, uint32_t vo, uint32_t so) {
+      ra[j] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, so, 0));
+    });
 #pragma unroll
-      for (int j = 0; j < RA; ++j) {
-        u4 v = {0u, 0u, 0u, 0u};
-        if (a_mask[j] && kin) v = *reinterpret_cast<const u4*>(a_ptr[j] + k);
-        ra[j] = v;
-      }
-    } else {
-      const ptrdiff_t delta = ((ptrdiff_t)rr * p.W + ss) * p.xc + ci;
-      const uint32_t bit = kin ? (1u << tap) : 0u;
-#pragma unroll
-      for (int j = 0; j < RA; ++j) {
-        u4 v = {0u, 0u, 0u, 0u};
-        if (a_mask[j] & bit) v = *reinterpret_cast<const u4*>(a_ptr[j] + delta);
-        ra[j] = v;
-      }
-      ci += BKE;  // advance to the next K step
-      while (ci >= p.cin) { ci -= p.cin; ++tap; if (++ss == p.k) { ss = 0; ++rr; } }
-    }
-#pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      u4 v = {0u, 0u, 0u, 0u};
-      if (b_ok[j]) v = *reinterpret_cast<const u4*>(b_ptr[j] + kt * BKE);
-      rb[j] = v;
-    }
+    for (int j = 0; j < RB; ++j)
+      rb[j] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(wr, b_off[j], (uint32_t)kt * BKE * 2, 0));
   };
-  auto lstore = [&](int buf) {
+  auto lstore = [&](int buf, const u4 (&ra)[RA], const u4 (&rb)[RB]) {
     unsigned char* As = smem + buf * STAGE;
     unsigned char* Bs = As + BM * ROWB;
 #pragma unroll
@@ -177,7 +191,7 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
 #pragma unroll
     for (int j = 0; j < RB; ++j) {
       const int row = r0 + 32 * j;
-      if (row < BN) *reinterpret_cast<u4*>(Bs + row * ROWB + swz(row, c) * 16) = rb[j];
+      if (BN % 32 == 0 || row < BN) *reinterpret_cast<u4*>(Bs + row * ROWB + swz(row, c) * 16) = rb[j];
     }
   };
 
@@ -193,12 +207,7 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
     for (int i = 0; i < TM; ++i) acc[j][i] = bv;
   }
 
-  gload(0);
-  lstore(0);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < nk) gload(kt + 1);
+  auto compute = [&](int buf) {
     const unsigned char* As = smem + buf * STAGE;
     const unsigned char* Bs = As + BM * ROWB;
 #pragma unroll
@@ -222,8 +231,36 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
           acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]),
                                                              __builtin_bit_cast(h8, xa[i]), acc[j][i], 0, 0, 0);
     }
-    if (kt + 1 < nk) lstore(buf ^ 1);
+  };
+
+  u4 ra[RA], rb[RB];
+  gload(0, ra, rb);
+  lstore(0, ra, rb);
+  if constexpr (PF == 1) {
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      if (kt + 1 < nk) gload(kt + 1, ra, rb);
+      compute(kt & 1);
+      if (kt + 1 < nk) lstore((kt & 1) ^ 1, ra, rb);
+      __syncthreads();
+    }
+  } else {
+    // two register sets: the loads of step kt+2 are issued before step kt's MFMAs and have two steps
+    // of MFMA work (instead of one) to land before their LDS write
+    u4 ra2[RA], rb2[RB];
+    if (nk > 1) gload(1, ra2, rb2);
+    __syncthreads();
+    for (int kt = 0; kt < nk; kt += 2) {
+      if (kt + 2 < nk) gload(kt + 2, ra, rb);
+      compute(0);
+      if (kt + 1 < nk) lstore(1, ra2, rb2);
+      __syncthreads();
+      if (kt + 1 >= nk) break;
+      if (kt + 3 < nk) gload(kt + 3, ra2, rb2);
+      compute(1);
+      if (kt + 2 < nk) lstore(0, ra, rb);
+      __syncthreads();
+    }
   }
 
   // accumulator acc[j][i][e]: output channel n = n0 + wn*WTN + j*16 + g*4 + e, pixel m = m0 + wm*WTM + i*16 + li
@@ -297,6 +334,17 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
     return;
   }
 
+  // output row table: element offset of each tile row's pixel in the bordered output (or ~0u past M)
+  uint32_t* yrow = reinterpret_cast<uint32_t*>(smem + BM * CPITCH);
+  if (tid < BM) {
+    const int m = m0 + tid;
+    uint32_t v = ~0u;
+    if (m < p.M) {
+      PixelWalk pw(p, m);
+      v = (uint32_t)(pix_index(pw.b, pw.ho, pw.wo, p.Ho, p.Wo) * p.yc + p.yoff);
+    }
+    yrow[tid] = v;
+  }
   unsigned char* Cs = smem;
   with_act(p.act, [&](auto actc) {
     constexpr int ACT = decltype(actc)::value;
@@ -319,23 +367,23 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   _Float16* __restrict__ y = reinterpret_cast<_Float16*>(p.y);
   for (int cc = tid; cc < BM * CPR; cc += NT) {
     const int row = cc / CPR, ch = cc - row * CPR;
-    const int m = m0 + row, n = n0 + ch * 8;
-    if (m < p.M && n < p.cout)
-      *reinterpret_cast<u4*>(y + (size_t)m * p.yc + p.yoff + n) = *reinterpret_cast<const u4*>(Cs + row * CPITCH + ch * 16);
+    const uint32_t yo = yrow[row];
+    const int n = n0 + ch * 8;
+    if (yo != ~0u && n < p.cout)
+      *reinterpret_cast<u4*>(y + yo + n) = *reinterpret_cast<const u4*>(Cs + row * CPITCH + ch * 16);
   }
 }
 
 // ---------------------------------------------------------------------------------------------
-// v4: 8-wave LDS-DMA ring (the main-path kernel for cout >= 64).
+// 8-wave LDS-DMA ring (wide layers).
 //  * 512 threads = 8 waves (2 per SIMD, so one wave's fragment reads hide under the other's MFMAs),
-//    BM x BN tile, BK = 64, STAGES-deep ring of LDS stages filled by global_load_lds_dwordx4 — no
-//    VGPR staging and no ds_write pass;
+//    BM x BN tile, BK = 64, STAGES-deep ring of LDS stages filled by buffer_load_dwordx4 ... lds —
+//    no VGPR staging and no ds_write pass;
 //  * each wave-instruction fills 8 tile rows (1 KiB, lane-linear in LDS), so the XOR swizzle is
 //    applied on the SOURCE chunk (c = slot ^ (row & 7)) and the ds_read side uses the same swz();
 //  * counted `s_waitcnt vmcnt(PER)` keeps the next stage in flight across a raw s_barrier (never
 //    __syncthreads in the loop: its fence would drain the DMA); the stage refilled at step kt is the
-//    one every wave finished reading at step kt-1 (its MFMAs consumed those reads before the barrier);
-//  * padding taps and rows beyond M / cout read a zeroed device page (LDS-DMA cannot zero-fill).
+//    one every wave finished reading at step kt-1 (its MFMAs consumed those reads before the barrier).
 template <int BM, int BN, int WM, int WN, int STAGES, bool ONE>
 __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 1024) ? 2 : 1) void conv_f16_ring_kernel(const ConvParams p) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
@@ -346,7 +394,8 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   constexpr int PER = RA + RB;
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int CPITCH = BN * 2 + 16;
-  constexpr int LDS = (STAGES * STAGE > BM * CPITCH) ? STAGES * STAGE : BM * CPITCH;
+  constexpr int EPI = BM * CPITCH + BM * 4;
+  constexpr int LDS = (STAGES * STAGE > EPI) ? STAGES * STAGE : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
@@ -361,79 +410,35 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   const int nN = (p.cout + BN - 1) / BN;
   const int m0 = (wgid / nN) * BM, n0 = (wgid % nN) * BN;
 
-  const _Float16* __restrict__ x = reinterpret_cast<const _Float16*>(p.x);
-  const _Float16* __restrict__ w = reinterpret_cast<const _Float16*>(p.w);
-  const _Float16* zero = reinterpret_cast<const _Float16*>(p.zero);
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto wr = make_rsrc(p.w, p.wbytes);
 
   const int lr = lane >> 3;            // row within the 8-row group (== row & 7)
   const int c = (lane & 7) ^ lr;       // source chunk this lane fetches
 
-  const _Float16* a_ptr[RA];
-  uint32_t a_mask[RA];
-  if (ONE) {
-#pragma unroll
-    for (int j = 0; j < RA; ++j) {
-      const int m = m0 + (j * NW + wave) * 8 + lr;
-      a_ptr[j] = x + (size_t)(m < p.M ? m : 0) * p.xc + p.xoff;
-      a_mask[j] = m < p.M ? 1u : 0u;
-    }
-  } else {
+  AWalk<ONE, RA> aw;
+  aw.init(p, c);
+  {
     PixelWalk pw(p, m0 + wave * 8 + lr);
 #pragma unroll
     for (int j = 0; j < RA; ++j) {
       if (j) pw.advance(p, NW * 8);
-      im2col_row(p, x, pw.b, pw.ho, pw.wo, m0 + (j * NW + wave) * 8 + lr < p.M, a_ptr[j], a_mask[j]);
+      aw.off[j] = a_origin(p, pw.b, pw.ho, pw.wo, c);
     }
   }
-  const _Float16* b_ptr[RB];
+  uint32_t b_off[RB];
 #pragma unroll
-  for (int j = 0; j < RB; ++j) {
-    const int row = (j * NW + wave) * 8 + lr;
-    b_ptr[j] = n0 + row < p.cout ? w + (size_t)(n0 + row) * p.kpad + c * 8 : nullptr;
-  }
+  for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)(((n0 + (j * NW + wave) * 8 + lr) * p.kpad + c * 8) * 2);
 
   const int nk = p.kpad / BKE;
-  int ci = c * 8, tap = 0, rr = 0, ss = 0;
-  if (!ONE) {
-    while (ci >= p.cin) { ci -= p.cin; ++tap; if (++ss == p.k) { ss = 0; ++rr; } }
-  }
-
   auto issue = [&](int kt, int slot) {
     unsigned char* As = smem + slot * STAGE;
     unsigned char* Bs = As + BM * ROWB;
-    const int k = kt * BKE + c * 8;
-    const bool kin = k < p.K;
-    if (ONE) {
+    aw.step(p, kt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * 8 * ROWB, vo, so); });
 #pragma unroll
-      for (int j = 0; j < RA; ++j) {
-        const _Float16* src = (a_mask[j] && kin) ? a_ptr[j] + k : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src,
-                                         (__attribute__((address_space(3))) void*)(As + (j * NW + wave) * 8 * ROWB),
-                                         16, 0, 0);
-      }
-    } else {
-      const ptrdiff_t delta = ((ptrdiff_t)rr * p.W + ss) * p.xc + ci;
-      const uint32_t bit = kin ? (1u << tap) : 0u;
-#pragma unroll
-      for (int j = 0; j < RA; ++j) {
-        const _Float16* src = (a_mask[j] & bit) ? a_ptr[j] + delta : zero;
-        __builtin_amdgcn_global_load_lds((const void*)src,
-                                         (__attribute__((address_space(3))) void*)(As + (j * NW + wave) * 8 * ROWB),
-                                         16, 0, 0);
-      }
-      ci += BKE;
-      while (ci >= p.cin) { ci -= p.cin; ++tap; if (++ss == p.k) { ss = 0; ++rr; } }
-    }
-#pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const _Float16* src = b_ptr[j] ? b_ptr[j] + kt * BKE : zero;
-      __builtin_amdgcn_global_load_lds((const void*)src,
-                                       (__attribute__((address_space(3))) void*)(Bs + (j * NW + wave) * 8 * ROWB),
-                                       16, 0, 0);
-    }
+    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * 8 * ROWB, b_off[j], (uint32_t)kt * BKE * 2);
   };
 
-  // accumulators start at the bias (one VALU add per output element less in the epilogue)
   f4 acc[TN][TM];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -492,6 +497,16 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
+  uint32_t* yrow = reinterpret_cast<uint32_t*>(smem + BM * CPITCH);
+  for (int t = tid; t < BM; t += NTH) {
+    const int m = m0 + t;
+    uint32_t v = ~0u;
+    if (m < p.M) {
+      PixelWalk pw(p, m);
+      v = (uint32_t)(pix_index(pw.b, pw.ho, pw.wo, p.Ho, p.Wo) * p.yc + p.yoff);
+    }
+    yrow[t] = v;
+  }
   unsigned char* Cs = smem;
   with_act(p.act, [&](auto actc) {
     constexpr int ACT = decltype(actc)::value;
@@ -514,9 +529,10 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   _Float16* __restrict__ y = reinterpret_cast<_Float16*>(p.y);
   for (int cc = tid; cc < BM * CPR; cc += NTH) {
     const int row = cc / CPR, ch = cc - row * CPR;
-    const int m = m0 + row, n = n0 + ch * 8;
-    if (m < p.M && n < p.cout)
-      *reinterpret_cast<u4*>(y + (size_t)m * p.yc + p.yoff + n) = *reinterpret_cast<const u4*>(Cs + row * CPITCH + ch * 16);
+    const uint32_t yo = yrow[row];
+    const int n = n0 + ch * 8;
+    if (yo != ~0u && n < p.cout)
+      *reinterpret_cast<u4*>(y + yo + n) = *reinterpret_cast<const u4*>(Cs + row * CPITCH + ch * 16);
   }
 }
 
@@ -532,10 +548,10 @@ hipError_t launch_ring2(const ConvParams& p, bool one, hipStream_t st) {
   return one ? launch_ring<BM, BN, WM, WN, STAGES, true>(p, st) : launch_ring<BM, BN, WM, WN, STAGES, false>(p, st);
 }
 
-template <int BM, int BN, int WM, bool ONE, bool DET>
+template <int BM, int BN, int WM, bool ONE, bool DET, int PF = 1>
 hipError_t launch_t(const ConvParams& p, hipStream_t st) {
   const int nM = (p.M + BM - 1) / BM, nN = (p.cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, ONE, DET>), dim3(nM * nN), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, ONE, DET, PF>), dim3(nM * nN), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 
@@ -545,7 +561,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   const bool one = p.k == 1 && p.s == 1 && p.pad == 0;
   static const int env_variant = [] { const char* e = getenv("YV7_CONV_F16"); return e ? atoi(e) : 0; }();
   const int variant = p.variant ? p.variant : env_variant;
-  if (!det && p.zero && p.cout > 32) {
+  if (!det && p.cout > 32) {
     if (variant == 4) {
       if (p.cout <= 64) return launch_ring2<256, 64, 4, 2, 3>(p, one, st);
       return launch_ring2<256, 128, 4, 2, 3>(p, one, st);
@@ -562,6 +578,10 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 7) {
       if (p.cout <= 64) return launch_ring2<128, 64, 2, 2, 4>(p, one, st);
       return launch_ring2<128, 128, 2, 2, 3>(p, one, st);
+    }
+    if (variant == 8) {
+      if (p.cout <= 64) return one ? launch_t<128, 64, 2, true, false, 2>(p, st) : launch_t<128, 64, 2, false, false, 2>(p, st);
+      return one ? launch_t<128, 128, 2, true, false, 2>(p, st) : launch_t<128, 128, 2, false, false, 2>(p, st);
     }
     if (variant == 0 && p.cout >= 256) {
       // wide layers: the 8-wave ring kernels win once their grid still covers the chip

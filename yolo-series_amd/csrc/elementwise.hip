@@ -26,20 +26,21 @@ template <> __device__ __forceinline__ _Float16 neg_inf<_Float16>() { return (_F
 
 template <typename T> __device__ __forceinline__ T tmax(T a, T b) { return a > b ? a : b; }
 
-// ---- input: x [B,3,H,W] (f32 or f16) -> NHWC T [B,H',W',yc], zero-padded channels.
+// Index math is 32-bit throughout (pixel and vector counts of one launch stay far below 2^31; the
+// runtime checks tensor sizes): a 64-bit division costs several times the 16-byte move it addresses.
+
+// ---- input: x [B,3,H,W] (f32 or f16) -> bordered NHWC T [B,H',W',yc], zero-padded channels.
 //      reorg: space-to-depth, channel = g*3 + c, g over (row even,col even),(odd,even),(even,odd),(odd,odd)
 template <typename T, typename S, bool REORG>
 __global__ __launch_bounds__(NT) void input_kernel(const S* __restrict__ x, T* __restrict__ y, int B, int H, int W,
                                                    int yc) {
   const int Ho = REORG ? H / 2 : H, Wo = REORG ? W / 2 : W;
-  const size_t npix = (size_t)B * Ho * Wo;
+  const int npix = B * Ho * Wo;
   const size_t plane = (size_t)H * W;
-  for (size_t pix = blockIdx.x * (size_t)NT + threadIdx.x; pix < npix; pix += (size_t)gridDim.x * NT) {
-    const int wo = (int)(pix % Wo);
-    const size_t t = pix / Wo;
-    const int ho = (int)(t % Ho);
-    const int b = (int)(t / Ho);
-    T* out = y + pix * yc;
+  for (int pix = blockIdx.x * NT + threadIdx.x; pix < npix; pix += gridDim.x * NT) {
+    const int t = pix / Wo, wo = pix - t * Wo;
+    const int b = t / Ho, ho = t - b * Ho;
+    T* out = y + pix_index(b, ho, wo, Ho, Wo) * yc;
     const S* xb = x + (size_t)b * 3 * plane;
     if (!REORG) {
       const size_t o = (size_t)ho * W + wo;
@@ -64,31 +65,28 @@ __global__ __launch_bounds__(NT) void maxpool_kernel(const T* __restrict__ x, in
                                                      int k, int s, int pad) {
   constexpr int V = Vec<T>::N;
   const int cv = C / V;
-  const size_t total = (size_t)B * Ho * Wo * cv;
-  for (size_t i = blockIdx.x * (size_t)NT + threadIdx.x; i < total; i += (size_t)gridDim.x * NT) {
-    const int c = (int)(i % cv) * V;
-    const size_t pix = i / cv;
-    const int wo = (int)(pix % Wo);
-    const size_t t = pix / Wo;
-    const int ho = (int)(t % Ho);
-    const int b = (int)(t / Ho);
+  const int total = B * Ho * Wo * cv;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int pix = i / cv, c = (i - pix * cv) * V;
+    const int t = pix / Wo, wo = pix - t * Wo;
+    const int b = t / Ho, ho = t - b * Ho;
     T m[V];
 #pragma unroll
     for (int e = 0; e < V; ++e) m[e] = neg_inf<T>();
     const int h0 = ho * s - pad, w0 = wo * s - pad;
-    for (int dy = 0; dy < k; ++dy) {
-      const int hi = h0 + dy;
-      if ((unsigned)hi >= (unsigned)H) continue;
-      for (int dx = 0; dx < k; ++dx) {
-        const int wi = w0 + dx;
-        if ((unsigned)wi >= (unsigned)W) continue;
-        const u4 v = *reinterpret_cast<const u4*>(x + (((size_t)b * H + hi) * W + wi) * xc + xoff + c);
+    // -inf padding (nn.MaxPool2d): taps outside the image are skipped, never read from the zero frame
+    const int ha = h0 < 0 ? 0 : h0, hb = h0 + k > H ? H : h0 + k;
+    const int wa = w0 < 0 ? 0 : w0, wb = w0 + k > W ? W : w0 + k;
+    for (int hi = ha; hi < hb; ++hi) {
+      const T* row = x + pix_index(b, hi, 0, H, W) * xc + xoff + c;
+      for (int wi = wa; wi < wb; ++wi) {
+        const u4 v = *reinterpret_cast<const u4*>(row + (size_t)wi * xc);
         const T* e = reinterpret_cast<const T*>(&v);
 #pragma unroll
         for (int q = 0; q < V; ++q) m[q] = tmax(m[q], e[q]);
       }
     }
-    *reinterpret_cast<u4*>(y + pix * yc + yoff + c) = *reinterpret_cast<const u4*>(m);
+    *reinterpret_cast<u4*>(y + pix_index(b, ho, wo, Ho, Wo) * yc + yoff + c) = *reinterpret_cast<const u4*>(m);
   }
 }
 
@@ -97,29 +95,28 @@ __global__ __launch_bounds__(NT) void upsample_kernel(const T* __restrict__ x, i
                                                       T* __restrict__ y, int yc, int yoff, int C) {
   constexpr int V = Vec<T>::N;
   const int cv = C / V, Ho = 2 * H, Wo = 2 * W;
-  const size_t total = (size_t)B * Ho * Wo * cv;
-  for (size_t i = blockIdx.x * (size_t)NT + threadIdx.x; i < total; i += (size_t)gridDim.x * NT) {
-    const int c = (int)(i % cv) * V;
-    const size_t pix = i / cv;
-    const int wo = (int)(pix % Wo);
-    const size_t t = pix / Wo;
-    const int ho = (int)(t % Ho);
-    const int b = (int)(t / Ho);
-    *reinterpret_cast<u4*>(y + pix * yc + yoff + c) =
-        *reinterpret_cast<const u4*>(x + (((size_t)b * H + (ho >> 1)) * W + (wo >> 1)) * xc + xoff + c);
+  const int total = B * Ho * Wo * cv;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int pix = i / cv, c = (i - pix * cv) * V;
+    const int t = pix / Wo, wo = pix - t * Wo;
+    const int b = t / Ho, ho = t - b * Ho;
+    *reinterpret_cast<u4*>(y + pix_index(b, ho, wo, Ho, Wo) * yc + yoff + c) =
+        *reinterpret_cast<const u4*>(x + pix_index(b, ho >> 1, wo >> 1, H, W) * xc + xoff + c);
   }
 }
 
 template <typename T>
-__global__ __launch_bounds__(NT) void copy_kernel(const T* __restrict__ x, size_t npix, int xc, int xoff,
+__global__ __launch_bounds__(NT) void copy_kernel(const T* __restrict__ x, int B, int H, int W, int xc, int xoff,
                                                   T* __restrict__ y, int yc, int yoff, int C) {
   constexpr int V = Vec<T>::N;
   const int cv = C / V;
-  const size_t total = npix * cv;
-  for (size_t i = blockIdx.x * (size_t)NT + threadIdx.x; i < total; i += (size_t)gridDim.x * NT) {
-    const int c = (int)(i % cv) * V;
-    const size_t pix = i / cv;
-    *reinterpret_cast<u4*>(y + pix * yc + yoff + c) = *reinterpret_cast<const u4*>(x + pix * xc + xoff + c);
+  const int total = B * H * W * cv;
+  for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
+    const int pix = i / cv, c = (i - pix * cv) * V;
+    const int t = pix / W, w = pix - t * W;
+    const int b = t / H, h = t - b * H;
+    const size_t q = pix_index(b, h, w, H, W);
+    *reinterpret_cast<u4*>(y + q * yc + yoff + c) = *reinterpret_cast<const u4*>(x + q * xc + xoff + c);
   }
 }
 
@@ -172,13 +169,12 @@ hipError_t launch_upsample2x(int dtype, const void* x, int B, int H, int W, int 
 
 hipError_t launch_copy(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int yc, int yoff,
                        int C, hipStream_t st) {
-  const size_t npix = (size_t)B * H * W;
-  const size_t work = npix * (C / (dtype == 1 ? 8 : 4));
+  const size_t work = (size_t)B * H * W * (C / (dtype == 1 ? 8 : 4));
   if (dtype == 1)
-    hipLaunchKernelGGL(copy_kernel<_Float16>, dim3(grid_for(work)), dim3(NT), 0, st, (const _Float16*)x, npix, xc,
+    hipLaunchKernelGGL(copy_kernel<_Float16>, dim3(grid_for(work)), dim3(NT), 0, st, (const _Float16*)x, B, H, W, xc,
                        xoff, (_Float16*)y, yc, yoff, C);
   else
-    hipLaunchKernelGGL(copy_kernel<float>, dim3(grid_for(work)), dim3(NT), 0, st, (const float*)x, npix, xc, xoff,
+    hipLaunchKernelGGL(copy_kernel<float>, dim3(grid_for(work)), dim3(NT), 0, st, (const float*)x, B, H, W, xc, xoff,
                        (float*)y, yc, yoff, C);
   return hipGetLastError();
 }

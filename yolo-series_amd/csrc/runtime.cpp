@@ -33,7 +33,10 @@ struct yv7_plan {
   std::vector<float> stride, anchor_grid;
   void* weights = nullptr;
   size_t wbytes = 0;
-  void* zero = nullptr;  // 4 KiB of zeros: source of LDS-DMA loads for padding taps / out-of-range rows
+  void* zero = nullptr;  // 4 KiB of zeros
+  // the workspace whose zero frames are known to be intact (see yv7_forward)
+  const void* ws_ready = nullptr;
+  size_t ws_ready_bytes = 0;
   // live profiling: events[f * (n_ops + 1) + i]
   std::vector<hipEvent_t> events;
   int prof_max = 0, prof_used = 0;
@@ -56,14 +59,18 @@ int hip_fail(hipError_t e, const char* where) {
 size_t elem_size(int dtype) { return dtype == YV7_DT_F16 ? 2 : 4; }
 size_t align256(size_t x) { return (x + 255) & ~(size_t)255; }
 
-// Byte offset of every tensor inside the workspace for a [B,3,H,W] batch.
+size_t tensor_bytes(const yv7_plan* p, const yv7_tensor_desc& t, int B, int H, int W) {
+  return yv7::bordered_pixels(B, H >> t.shift, W >> t.shift) * t.channels * elem_size(p->dtype);
+}
+
+// Byte offset of every tensor inside the workspace for a [B,3,H,W] batch: bordered NHWC
+// [B][h + 2*YV7_BORDER][w + 2*YV7_BORDER][C] each, 256-byte aligned.
 std::vector<size_t> tensor_offsets(const yv7_plan* p, int B, int H, int W, size_t* total) {
   std::vector<size_t> off(p->tensors.size());
   size_t o = 0;
   for (size_t i = 0; i < p->tensors.size(); ++i) {
-    const auto& t = p->tensors[i];
     off[i] = o;
-    o = align256(o + (size_t)B * (H >> t.shift) * (W >> t.shift) * t.channels * elem_size(p->dtype));
+    o = align256(o + tensor_bytes(p, p->tensors[i], B, H, W));
   }
   *total = o;
   return off;
@@ -75,6 +82,10 @@ int check_hw(const yv7_plan* p, int B, int H, int W) {
     return fail(YV7_E_SHAPE, "input H and W must be positive multiples of " + std::to_string(1 << p->max_shift) +
                                  " (got B=" + std::to_string(B) + " H=" + std::to_string(H) + " W=" +
                                  std::to_string(W) + ")");
+  // kernels address a tensor with 32-bit byte offsets (buffer loads)
+  for (const auto& t : p->tensors)
+    if (tensor_bytes(p, t, B, H, W) >= (size_t(1) << 31))
+      return fail(YV7_E_SHAPE, "batch too large: an activation tensor would exceed 2 GiB (split the batch)");
   return 0;
 }
 
@@ -114,6 +125,9 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
       if (o.w_off < 0 || o.b_off < 0 || (size_t)o.w_off + wb > nbytes ||
           (size_t)o.b_off + sizeof(float) * o.cout > nbytes)
         return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " weight range outside blob");
+      if (o.k < 1 || o.s < 1 || o.pad < 0 || o.pad > YV7_BORDER || o.k - 1 - o.pad > YV7_BORDER)
+        return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) +
+                                   " window reaches past the tensors' zero frame (needs pad <= 1, k - 1 - pad <= 1)");
       if (o.kind == YV7_OP_DETECT && (o.level < 0 || o.level >= d->nl || o.cout != d->na * d->no || o.k != 1))
         return fail(YV7_E_ARG, "yv7_plan_create: bad detect op");
     }
@@ -250,8 +264,8 @@ int yv7_tensor_info(const yv7_plan* p, int id, int B, int H, int W, int64_t* off
   *offset = (int64_t)off[id];
   const auto& t = p->tensors[id];
   dims4[0] = B;
-  dims4[1] = H >> t.shift;
-  dims4[2] = W >> t.shift;
+  dims4[1] = (H >> t.shift) + 2 * YV7_BORDER;
+  dims4[2] = (W >> t.shift) + 2 * YV7_BORDER;
   dims4[3] = t.channels;
   return 0;
 }
@@ -268,6 +282,14 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   unsigned char* wsb = reinterpret_cast<unsigned char*>(ws);
   const unsigned char* wb = reinterpret_cast<const unsigned char*>(p->weights);
+  hipError_t e = hipSuccess;
+  // Kernels write only tensor interiors, so the zero frames survive from one forward to the next:
+  // the workspace is cleared when it is first seen (or its layout changes) and never again.
+  if (ws != p->ws_ready || total != p->ws_ready_bytes) {
+    if ((e = hipMemsetAsync(ws, 0, total, st)) != hipSuccess) return hip_fail(e, "hipMemsetAsync(workspace)");
+    p->ws_ready = ws;
+    p->ws_ready_bytes = total;
+  }
   const size_t es = elem_size(p->dtype);
   const int nrows = (int)yv7_num_rows(p, H, W);
   // raw-logit and z row offsets of each level
@@ -289,7 +311,6 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
       racc += (size_t)B * lvl_rows[l] * p->no;
     }
   }
-  hipError_t e = hipSuccess;
   hipEvent_t* ev = nullptr;
   if (p->prof_used < p->prof_max) {
     ev = &p->events[(size_t)p->prof_used * (p->ops.size() + 1)];
@@ -329,6 +350,8 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
         c.w = wb + o.w_off;
         c.bias = reinterpret_cast<const float*>(wb + o.b_off);
         c.zero = p->zero;
+        c.xbytes = (uint32_t)tensor_bytes(p, ti, B, H, W);
+        c.wbytes = (uint32_t)((size_t)((o.cout + 31) / 32 * 32) * c.kpad * es);
         if (o.kind == YV7_OP_CONV) {
           const auto& to = p->tensors[o.dst];
           if (c.Ho != (H >> to.shift) || c.Wo != (W >> to.shift))
@@ -407,7 +430,6 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
     if (e != hipSuccess) return hip_fail(e, "yv7_forward launch");
     if (ev && (e = hipEventRecord(ev[i + 1], st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
-  (void)es;
   return 0;
 }
 

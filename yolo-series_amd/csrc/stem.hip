@@ -176,7 +176,7 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
     const int ty = mb / TBX, tx = mb - ty * TBX;
     const int oy = oy0 + ty, ox = ox0 + tx;
     if (oy < HB && ox < WB)
-      *reinterpret_cast<u4*>(y + (((size_t)b * HB + oy) * WB + ox) * p.yc + p.yoff + ch * 8) =
+      *reinterpret_cast<u4*>(y + pix_index(b, oy, ox, HB, WB) * p.yc + p.yoff + ch * 8) =
           *reinterpret_cast<const u4*>(smem + mb * CPITCH + ch * 16);
   }
 }

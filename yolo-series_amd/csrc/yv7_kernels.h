@@ -34,14 +34,34 @@ __device__ __forceinline__ void with_act(int act, F&& f) {
   else f(std::integral_constant<int, 0>{});
 }
 
+// Activation tensors in the workspace are NHWC with a BORDER-pixel zero frame around every image:
+// [B][H + 2*BORDER][W + 2*BORDER][C], kernels write only the interior.  A 3x3 / pad-1 window then never
+// needs a bounds test (its out-of-image taps read the zero frame), so the conv kernels' operand loads
+// are unconditional buffer loads with the tap offset in a scalar register.
+constexpr int BORDER = 1;
+
+// Element index of pixel (b, h, w) (interior coordinates, -BORDER <= h < H + BORDER) of a bordered tensor.
+__host__ __device__ __forceinline__ size_t pix_index(int b, int h, int w, int H, int W) {
+  return ((size_t)b * (H + 2 * BORDER) + h + BORDER) * (W + 2 * BORDER) + w + BORDER;
+}
+__host__ __device__ __forceinline__ size_t bordered_pixels(int B, int H, int W) {
+  return (size_t)B * (H + 2 * BORDER) * (W + 2 * BORDER);
+}
+
+// Raw buffer resource over [base, base + bytes): loads at voffset >= bytes return zero.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* base, uint32_t bytes) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(base), (short)0, (int)bytes, 0x00020000);
+}
+
 // Kernel parameters of one conv launch (also the fused Detect head).
 struct ConvParams {
-  const void* x;      // NHWC input tensor base
-  void* y;            // NHWC output tensor base (CONV)
+  const void* x;      // bordered NHWC input tensor (allocation start)
+  void* y;            // bordered NHWC output tensor (CONV)
   const void* w;      // packed weights [cout_pad][kpad]
   const float* bias;  // [cout_pad]
-  const void* zero;   // >= 16 zero bytes in device memory (LDS-DMA source for padding / out-of-range)
-  int B, H, W, xc, xoff, cin;       // input geometry, pitch (channels), channel offset, channels read
+  const void* zero;   // >= 16 zero bytes in device memory
+  uint32_t xbytes, wbytes;          // byte sizes of the input tensor / this conv's weights (buffer ranges)
+  int B, H, W, xc, xoff, cin;       // input geometry (interior), pitch (channels), channel offset, channels read
   int Ho, Wo, yc, yoff, cout;       // output geometry
   int k, s, pad, act, kpad, K, M;   // K = k*k*cin, M = B*Ho*Wo
   // Detect epilogue
@@ -55,7 +75,7 @@ struct ConvParams {
 // Fused stem: image -> conv A (3 -> 32, 3x3, stride sa) -> conv B (32 -> 64, 3x3, stride 2).
 struct StemParams {
   const void* x;        // [B,3,H,W] image (fp16 or fp32)
-  void* y;              // conv-B output tensor base (NHWC fp16)
+  void* y;              // conv-B output tensor (bordered NHWC fp16)
   const void* wa;       // conv-A weights [32][kpad_a] (k = tap*3 + ci)
   const float* ba;
   const void* wb;       // conv-B weights [64][kpad_b] (k = tap*32 + ci)

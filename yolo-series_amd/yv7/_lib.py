@@ -13,7 +13,8 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libyv7.so')
 
-ABI_VERSION = 1
+ABI_VERSION = 2
+BORDER = 1          # zero frame around every workspace tensor (YV7_BORDER)
 DT_F32, DT_F16 = 0, 1
 ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
 OP_INPUT, OP_CONV, OP_MAXPOOL, OP_UPSAMPLE, OP_COPY, OP_DETECT, OP_STEM = 0, 1, 2, 3, 4, 5, 6

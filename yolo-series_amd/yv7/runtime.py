@@ -85,7 +85,8 @@ class Plan:
         es = 2 if self.dtype == L.DT_F16 else 4
         n = dims[0] * dims[1] * dims[2] * dims[3]
         t = ws[off.value:off.value + n * es].view(torch.float16 if es == 2 else torch.float32)
-        return t.view(dims[0], dims[1], dims[2], dims[3])
+        bd = L.BORDER   # bordered layout (include/yv7.h YV7_BORDER): return the image interior
+        return t.view(dims[0], dims[1], dims[2], dims[3])[:, bd:dims[1] - bd, bd:dims[2] - bd]
 
     def layer_output(self, layer_i, B, H, W):
         """NCHW fp32 copy of layer `layer_i`'s output from the last forward."""
