@@ -562,6 +562,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   static const int env_variant = [] { const char* e = getenv("YV7_CONV_F16"); return e ? atoi(e) : 0; }();
   const int variant = p.variant ? p.variant : env_variant;
   if (!det && p.cout > 32) {
+    if ((variant == 0 || variant == 10) && halo_supported(p)) return launch_conv_halo(p, st);
     if (variant == 4) {
       if (p.cout <= 64) return launch_ring2<256, 64, 4, 2, 3>(p, one, st);
       return launch_ring2<256, 128, 4, 2, 3>(p, one, st);

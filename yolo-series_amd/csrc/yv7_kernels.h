@@ -86,6 +86,8 @@ struct StemParams {
 // Host launchers (defined in the .hip files, called from the runtime).
 hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t st);
 hipError_t launch_conv_f16(const ConvParams& p, bool detect, hipStream_t st);
+bool halo_supported(const ConvParams& p);
+hipError_t launch_conv_halo(const ConvParams& p, hipStream_t st);
 hipError_t launch_input(int dtype, const void* x, int x_dtype, void* y, int B, int H, int W, int yc,
                         bool reorg, hipStream_t st);
 hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int Ho,
