@@ -109,10 +109,11 @@ def main():
     det = torch.empty((B, 300, 6), dtype=torch.float32, device=dev)
     src = torch.empty((B, 300), dtype=torch.int64, device=dev)
     cnt = torch.empty((B,), dtype=torch.int32, device=dev)
+    rowbest = torch.empty((B, N, 4), dtype=torch.float32, device=dev)   # yv7_row_best records
 
     def step():
-        plan.forward_into(x, z)
-        nms_batched(z, 0.25, 0.45, out=(det, src, cnt))
+        plan.forward_into(x, z, rowbest=rowbest)
+        nms_batched(z, 0.25, 0.45, out=(det, src, cnt), rowbest=rowbest)
         if distributed:
             ydist.gather_detections(det, src, cnt)
 

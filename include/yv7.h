@@ -106,11 +106,23 @@ size_t yv7_workspace_bytes(const yv7_plan* plan, int B, int H, int W);
 /* Rows of z per image: sum over levels of na * (H >> s_l) * (W >> s_l). */
 int64_t yv7_num_rows(const yv7_plan* plan, int H, int W);
 
+/* Per-row detection score record (16 bytes), one per row of z: the objectness z[..., 4], the
+ * single-label NMS score max_c z[..., 5 + c] * z[..., 4] with its first-max class (general.py:669-684,
+ * computed from the very floats written to z).  yv7_nms / yv7_end2end accept it instead of
+ * re-reading every row of z for the candidate filter. */
+typedef struct {
+  float obj;
+  float conf;
+  int32_t cls;
+  int32_t reserved;
+} yv7_row_best;
+
 /* x: [B,3,H,W] (x_dtype f32 or f16, values in [0,1]) on the plan's device.
  * z_out: [B, N, no] fp32 decoded boxes (Detect z).  raw_out (nullable): per level l the raw head
- * logits [B, na, ny_l, nx_l, no] fp32, levels concatenated.  Asynchronous on `stream`. */
+ * logits [B, na, ny_l, nx_l, no] fp32, levels concatenated.  rowbest_out (nullable): [B, N]
+ * yv7_row_best (fp16 plans write it from the head's epilogue).  Asynchronous on `stream`. */
 int yv7_forward(yv7_plan* plan, const void* x, int x_dtype, int B, int H, int W, float* z_out,
-                float* raw_out, void* workspace, size_t ws_bytes, void* stream);
+                float* raw_out, yv7_row_best* rowbest_out, void* workspace, size_t ws_bytes, void* stream);
 
 /* Live per-op timing: with max_forwards > 0 every following yv7_forward (up to max_forwards of
  * them) records one HIP event before its first op and one after each op on its stream; 0 turns it
@@ -127,11 +139,13 @@ int yv7_tensor_info(const yv7_plan* plan, int tensor_id, int B, int H, int W, in
 
 /* Batched NMS over z [B,N,no] fp32, the semantics of utils/general.py:628-720.
  * det: [B,max_det,6] (x1,y1,x2,y2,conf,cls), src_row: [B,max_det] int64 anchor row of each kept
- * box, count: [B] int32.  classes: nullable [ncls] int32 class filter. */
+ * box, count: [B] int32.  classes: nullable [ncls] int32 class filter.  rowbest (nullable): the
+ * yv7_row_best records of z from yv7_forward; used for the single-label, unfiltered case. */
 size_t yv7_nms_workspace_bytes(int B, int N, int no, int multi_label, int max_nms);
-int yv7_nms(const float* z, int B, int N, int no, float conf_thres, float iou_thres, int multi_label,
-            int agnostic, const int32_t* classes, int ncls, int max_det, int max_nms, float* det,
-            int64_t* src_row, int32_t* count, void* workspace, size_t ws_bytes, void* stream);
+int yv7_nms(const float* z, const yv7_row_best* rowbest, int B, int N, int no, float conf_thres,
+            float iou_thres, int multi_label, int agnostic, const int32_t* classes, int ncls, int max_det,
+            int max_nms, float* det, int64_t* src_row, int32_t* count, void* workspace, size_t ws_bytes,
+            void* stream);
 
 /* EfficientNMS_TRT-shaped output (End2End, experimental.py:226-241): num_dets int32 [B,1],
  * det_boxes [B,topk,4], det_scores [B,topk], det_classes int32 [B,topk]; zero-padded. */

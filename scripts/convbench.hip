@@ -37,6 +37,9 @@ int main(int argc, char** argv) {
     {"1x1 128->64 @160", 32, 160, 160, 128, 64, 1, 1},
     {"1x1 512->512 @80", 32, 80, 80, 512, 512, 1, 1},
     {"1x1 1024->1024 @40", 32, 40, 40, 1024, 1024, 1, 1},
+    {"1x1 512->256 @80", 32, 80, 80, 512, 256, 1, 1},
+    {"1x1 1024->256 @40", 32, 40, 40, 1024, 256, 1, 1},
+    {"1x1 256->128 @160", 32, 160, 160, 256, 128, 1, 1},
     {"GEMM 4096^2 K4096", 32, 32, 32, 4096, 4096, 1, 1},
   };
   std::vector<int> variants;

@@ -46,7 +46,7 @@ def test_abi_version_and_host_only_entry_points():
     d.abi_version = 999
     rc = L.yv7_plan_create(ctypes.byref(d), None, 0, 0, ctypes.byref(ctypes.c_void_p()))
     assert rc == -4 and b'abi_version' in L.yv7_last_error()
-    rc = L.yv7_nms(None, 1, 10, 85, 0.25, 0.45, 0, 0, None, 0, 300, 30000, None, None, None, None, 0, None)
+    rc = L.yv7_nms(None, None, 1, 10, 85, 0.25, 0.45, 0, 0, None, 0, 300, 30000, None, None, None, None, 0, None)
     assert rc == -1
 
 

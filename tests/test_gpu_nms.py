@@ -136,3 +136,33 @@ def test_end2end_format():
                 iou = box_iou(boxes[b, idx], boxes[b, idx])
                 iou.fill_diagonal_(0)
                 assert iou.max() <= 0.45 + 1e-6
+
+
+def test_row_scores_from_head_epilogue():
+    """fp16 plan: the head epilogue's yv7_row_best records equal what NMS would compute from z
+    (same floats: objectness, first-max obj*cls score, class), NMS through them is bit-identical to
+    the oracle NMS on that z, and an in-place edit of z retires the records."""
+    from oracle import nms_ref
+    from utils.general import non_max_suppression
+    from yv7.runtime import row_scores
+    m = fresh_model('yolov7').to(DEV).half()
+    z, _ = m(frames(2, 640, 640, seed=8).to(DEV).half())
+    rb = row_scores.lookup(z)
+    assert rb is not None
+    zc, rbc = z.cpu(), rb.cpu()
+    obj = zc[..., 4]
+    sc = zc[..., 5:] * obj[..., None]
+    best, cls = sc.max(-1)
+    assert torch.equal(rbc[..., 0], obj)
+    assert torch.equal(rbc[..., 1], best)
+    assert torch.equal(rbc[..., 2].view(torch.int32), cls.to(torch.int32))
+    out_g, rows_g = non_max_suppression(z, 0.25, 0.45, return_rows=True)
+    out_x, rows_x = nms_ref.non_max_suppression(zc, 0.25, 0.45, return_rows=True)
+    for i in range(2):
+        assert torch.equal(rows_g[i].cpu(), rows_x[i]) and torch.equal(out_g[i].cpu(), out_x[i])
+    z[:, :, 4] *= 0.5                      # in-place edit: the records no longer describe z
+    assert row_scores.lookup(z) is None
+    out_g, rows_g = non_max_suppression(z, 0.25, 0.45, return_rows=True)
+    out_x, rows_x = nms_ref.non_max_suppression(z.cpu(), 0.25, 0.45, return_rows=True)
+    for i in range(2):
+        assert torch.equal(rows_g[i].cpu(), rows_x[i]) and torch.equal(out_g[i].cpu(), out_x[i])

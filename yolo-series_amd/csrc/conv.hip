@@ -257,9 +257,16 @@ hipError_t launch_dt(const ConvParams& p, bool det, hipStream_t st) {
 
 }  // namespace
 
+static bool use_v1() {
+  static const bool v1 = [] { const char* e = getenv("YV7_CONV_V1"); return e && e[0] == '1'; }();
+  return v1;
+}
+
+bool det_writes_rowbest(int dtype) { return dtype == 1 && !use_v1(); }
+
 hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t st) {
   // fp16: the tuned kernel of conv_f16.hip (YV7_CONV_V1=1 selects this file's generic kernel, for A/B)
-  static const bool v1 = [] { const char* e = getenv("YV7_CONV_V1"); return e && e[0] == '1'; }();
+  const bool v1 = use_v1();
   // cout <= 32 (the stem of every model, tiny's narrow layers): this kernel's BK=32 steps waste less
   // of the short, padded K than the 64-deep steps of conv_f16 (measured: scripts/convbench.hip)
   if (dtype == 1)

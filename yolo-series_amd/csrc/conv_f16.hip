@@ -299,6 +299,34 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
       gys[tid] = (float)gy;
     }
     __syncthreads();
+    // per-row NMS scores (yv7_row_best): objectness, first-max class score obj * cls_c, class — from
+    // the same sigmoid values the z rows below receive
+    if (p.best) {
+      for (int t = tid; t < BM * p.na; t += NT) {
+        const int pr = t % BM, a = t / BM;
+        const long long zr = zrow0[pr];
+        if (zr < 0) continue;
+        const float* lg = reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(Ds) + pr * DPITCH) +
+                          a * p.no;
+        auto sig = [](float v) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v)); };
+        const float obj = sig(lg[4]);
+        float best = obj;
+        int bc = 0;
+        if (p.no > 6) {
+          best = sig(lg[5]) * obj;
+          for (int c = 1; c < p.no - 5; ++c) {
+            const float v = sig(lg[5 + c]) * obj;
+            if (v > best) { best = v; bc = c; }   // strict >: the first maximum wins (general.py:683-684)
+          }
+        }
+        f4 rec;
+        rec[0] = obj;
+        rec[1] = best;
+        rec[2] = __builtin_bit_cast(float, bc);
+        rec[3] = 0.0f;
+        *reinterpret_cast<f4*>(p.best + (size_t)(zr + (long long)a * hw) * 4) = rec;
+      }
+    }
     // thread t walks e = t, t + NT, ... over the [BM][no] elements of one anchor: pr = e / no, o = e % no
     const int NO = p.no, step_pr = NT / NO, step_o = NT - step_pr * NO;
     for (int a = 0; a < p.na; ++a) {

@@ -2,7 +2,8 @@
 // torchvision.ops.nms call (general.py:704) restated as a blocked greedy scan.
 //
 // Pipeline (all images of the batch in one launch per stage, no host sync):
-//   1 nms_rows     one wave per anchor row: obj > conf (:637,:653), conf = cls*obj (:669-673),
+//   1 nms_rows     a lane per anchor row for obj > conf (:637,:653), then a wave per surviving row:
+//                  conf = cls*obj (:669-673),
 //                  single-label first-max argmax (:683-684) or multi-label class mask (:680-681),
 //                  optional class filter (:687-688) -> per-row candidate count (+best conf/cls)
 //   2 nms_scan     per-image exclusive scan of the counts -> stable row-order offsets
@@ -11,8 +12,9 @@
 //   4 nms_sort     per-image sort by (score desc, candidate index asc) == torchvision's stable
 //                  descending sort; bitonic in LDS up to 16384 candidates, in global memory above;
 //                  the first max_nms (:698-699) go on
-//   5 nms_greedy   blocked greedy NMS on class-offset boxes (:702-703, max_wh 4096): a wave resolves
-//                  64 sorted candidates at a time, the workgroup then strikes later candidates that
+//   5 nms_greedy   blocked greedy NMS on class-offset boxes (:702-703, max_wh 4096): per block of 64
+//                  sorted candidates the workgroup builds the 64 x 64 "i suppresses j" bitmask, one
+//                  wave resolves it with bit operations, the workgroup then strikes later candidates that
 //                  a box kept in that block overlaps (IoU > thr); stops at max_det kept (:705-706).
 // IoU arithmetic is torchvision's: area=(x2-x1)*(y2-y1), inter=max(0,.)*max(0,.),
 // inter / (area_i + area_j - inter) > thr, all fp32; this file is built with -ffp-contract=off.
@@ -67,27 +69,39 @@ __device__ __forceinline__ bool class_ok(const NmsArgs& a, int c) {
   return false;
 }
 
-// Stage 1: one wave per row. Lanes hold classes c and c+64.
+// Stage 1: a wave takes 64 rows at a time.  Each lane gathers one row's objectness; the rows above
+// conf (a few per 64) are then scored one after the other by the whole wave, lanes holding classes
+// c and c + 64, so the wave pays one memory latency per candidate row instead of one per row.
 __global__ __launch_bounds__(NT) void nms_rows(const NmsArgs a) {
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63;
   const int wave = (blockIdx.x * NT + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * NT) >> 6;
-  for (int row = wave; row < a.N; row += nwaves) {
-    const float* zr = a.z + ((size_t)b * a.N + row) * a.no;
-    const float obj = zr[4];
-    int cnt = 0;
-    float best = 0.f;
-    int bc = 0;
-    if (obj > a.conf) {
-      float v0 = -1.f, v1 = -1.f;
+  const float* zb = a.z + (size_t)b * a.N * a.no;
+  for (int r0 = wave * 64; r0 < a.N; r0 += nwaves * 64) {
+    const int myrow = r0 + lane;
+    const float myobj = myrow < a.N ? zb[(size_t)myrow * a.no + 4] : 0.f;
+    int mycnt = 0;
+    float mybest = 0.f;
+    int mycls = 0;
+    uint64_t pass = __ballot(myrow < a.N && myobj > a.conf);
+    while (pass) {
+      const int k = __ffsll((long long)pass) - 1;
+      pass &= pass - 1;
+      const int row = r0 + k;
+      const float* zr = zb + (size_t)row * a.no;
+      const float obj = __shfl(myobj, k);
       const int c0 = lane, c1 = lane + 64;
+      float v0 = -1.f, v1 = -1.f;
       if (a.nc == 1) {
         v0 = (c0 == 0) ? obj : -1.f;  // nc == 1: conf = obj (:669-670)
       } else {
         if (c0 < a.nc) v0 = zr[5 + c0] * obj;
         if (c1 < a.nc) v1 = zr[5 + c1] * obj;
       }
+      int cnt;
+      float best = 0.f;
+      int bc = 0;
       if (a.multi) {
         const bool p0 = c0 < a.nc && v0 > a.conf && class_ok(a, c0);
         const bool p1 = c1 < a.nc && v1 > a.conf && class_ok(a, c1);
@@ -107,15 +121,70 @@ __global__ __launch_bounds__(NT) void nms_rows(const NmsArgs a) {
         bc = c;
         cnt = (v > a.conf && class_ok(a, c)) ? 1 : 0;
       }
-    }
-    if (lane == 0) {
-      const size_t i = (size_t)b * a.N + row;
-      a.cnt[i] = cnt;
-      if (!a.multi) {
-        a.bconf[i] = best;
-        a.bcls[i] = bc;
+      if (lane == k) {
+        mycnt = cnt;
+        mybest = best;
+        mycls = bc;
       }
     }
+    if (myrow < a.N) {
+      const size_t i = (size_t)b * a.N + myrow;
+      a.cnt[i] = mycnt;
+      if (!a.multi) {
+        a.bconf[i] = mybest;
+        a.bcls[i] = mycls;
+      }
+    }
+  }
+}
+
+// yv7_row_best (include/yv7.h): the head epilogue's per-row scores.
+struct RowBest {
+  float obj, conf;
+  int cls, reserved;
+};
+
+// Stage 1 from row scores (single-label, no class filter): a 16-byte read per row instead of z.
+__global__ __launch_bounds__(NT) void nms_rows_from_best(const NmsArgs a, const RowBest* __restrict__ rb) {
+  const int b = blockIdx.y;
+  for (int row = blockIdx.x * NT + threadIdx.x; row < a.N; row += gridDim.x * NT) {
+    const size_t i = (size_t)b * a.N + row;
+    const RowBest r = rb[i];
+    const bool c = r.obj > a.conf && r.conf > a.conf;
+    a.cnt[i] = c ? 1 : 0;
+    a.bconf[i] = c ? r.conf : 0.f;
+    a.bcls[i] = c ? r.cls : 0;
+  }
+}
+
+// Row scores from z (for plans whose head kernel does not write them): a wave per 64 rows, every
+// row scored (the threshold is not known yet), classes c and c + 64 per lane.
+__global__ __launch_bounds__(NT) void row_best_kernel(const float* __restrict__ z, int N, int no, RowBest* __restrict__ out) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wave = (blockIdx.x * NT + threadIdx.x) >> 6;
+  const int nwaves = (gridDim.x * NT) >> 6;
+  const int nc = no - 5;
+  for (int row = wave; row < N; row += nwaves) {
+    const float* zr = z + ((size_t)b * N + row) * no;
+    const float obj = zr[4];
+    float v = -2.f;
+    int c = 1 << 30;
+    if (nc == 1) {
+      if (lane == 0) { v = obj; c = 0; }
+    } else {
+      if (lane < nc) { v = zr[5 + lane] * obj; c = lane; }
+      if (lane + 64 < nc) {
+        const float v1 = zr[5 + lane + 64] * obj;
+        if (v1 > v) { v = v1; c = lane + 64; }
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const float ov = __shfl_xor(v, off);
+      const int oc = __shfl_xor(c, off);
+      if (ov > v || (ov == v && oc < c)) { v = ov; c = oc; }
+    }
+    if (lane == 0) out[(size_t)b * N + row] = RowBest{obj, v, c, 0};
   }
 }
 
@@ -269,6 +338,7 @@ __global__ __launch_bounds__(SORT_T) void nms_greedy(const NmsArgs a) {
   float* karea = reinterpret_cast<float*>(kbox + 64);
   int* kcls = reinterpret_cast<int*>(karea + 64);
   __shared__ int nk_blk, total;
+  __shared__ uint64_t sup[64];
 
   // gather boxes in sorted order (class-offset unless agnostic / per-class)
   for (int i = threadIdx.x; i < n; i += SORT_T) {
@@ -286,8 +356,40 @@ __global__ __launch_bounds__(SORT_T) void nms_greedy(const NmsArgs a) {
   if (threadIdx.x == 0) total = 0;
   __syncthreads();
 
-  const int lane = threadIdx.x & 63;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int NW = SORT_T / 64;
   for (int base = 0; base < n; base += 64) {
+    // (a) every wave: for its rows i of this 64-candidate block, the 64-bit mask of later block
+    //     members j that i would suppress (IoU > thr, same class when per_class) -> sup[i] in LDS
+    {
+      const int j = base + lane;
+      const bool valid = j < n;
+      float4 bj = make_float4(0.f, 0.f, 0.f, 0.f);
+      float aj = 0.f;
+      int cj = -1;
+      if (valid) {
+        bj = sbox[j];
+        aj = sarea[j];
+        if (a.per_class) cj = cand[order[j]].cls;
+      }
+#pragma unroll
+      for (int q = 0; q < 64 / NW; ++q) {
+        const int i = wv * (64 / NW) + q;
+        const int ig = base + i;
+        bool hit = false;
+        if (ig < n && valid && lane > i) {
+          const float4 bi = sbox[ig];
+          const float ai = sarea[ig];
+          const int ci = a.per_class ? cand[order[ig]].cls : -1;
+          hit = (!a.per_class || ci == cj) && iou_gt(bi, ai, bj, aj, a.iou);
+        }
+        const uint64_t m = __ballot(hit);
+        if (lane == 0) sup[i] = m;
+      }
+    }
+    __syncthreads();
+    // (b) wave 0 resolves the block with bit operations: walk the alive candidates in sorted order;
+    //     each one still alive is kept and removes the later members it suppresses
     if (threadIdx.x < 64) {
       const int j = base + lane;
       const bool valid = j < n;
@@ -299,17 +401,14 @@ __global__ __launch_bounds__(SORT_T) void nms_greedy(const NmsArgs a) {
         aj = sarea[j];
         if (a.per_class) cj = cand[order[j]].cls;
       }
-      bool rem = !valid || ((removed[j >> 5] >> (j & 31)) & 1u);
-      uint64_t kept = 0;
+      const bool rem = !valid || ((removed[j >> 5] >> (j & 31)) & 1u);
+      const uint64_t my_sup = sup[lane];
       uint64_t alive = __ballot(!rem);
+      uint64_t kept = 0;
       while (alive) {
         const int i = __ffsll((long long)alive) - 1;
         kept |= 1ull << i;
-        const float4 bi = make_float4(__shfl(bj.x, i), __shfl(bj.y, i), __shfl(bj.z, i), __shfl(bj.w, i));
-        const float ai = __shfl(aj, i);
-        const int ci = __shfl(cj, i);
-        if (lane > i && !rem && (!a.per_class || ci == cj) && iou_gt(bi, ai, bj, aj, a.iou)) rem = true;
-        alive = (i == 63) ? 0ull : (__ballot(!rem) & ~((2ull << i) - 1ull));
+        alive &= ~__shfl(my_sup, i) & ~(1ull << i);
       }
       const int nk = __popcll(kept);
       const bool mine = (kept >> lane) & 1ull;
@@ -341,7 +440,6 @@ __global__ __launch_bounds__(SORT_T) void nms_greedy(const NmsArgs a) {
     // strike later candidates overlapped by a box kept in this block: one candidate per lane, each
     // wave owns whole 64-candidate chunks (two bitmap words), so no atomics are needed
     if (nk > 0) {
-      const int wv = threadIdx.x >> 6;
       for (int c0 = base + 64 + wv * 64; c0 < n; c0 += (SORT_T / 64) * 64) {
         const int j = c0 + lane;
         bool hit = false;
@@ -413,6 +511,13 @@ __global__ __launch_bounds__(NT) void end2end_pack(const float* det, const int32
 
 }  // namespace
 
+hipError_t launch_row_best(const float* z, int B, int N, int no, void* rowbest, hipStream_t st) {
+  int gx = (N + 31) / 32;
+  if (gx > 1024) gx = 1024;
+  hipLaunchKernelGGL(row_best_kernel, dim3(gx, B), dim3(NT), 0, st, z, N, no, reinterpret_cast<RowBest*>(rowbest));
+  return hipGetLastError();
+}
+
 hipError_t launch_end2end_pack(const float* det, const int32_t* count, int B, int max_det, int topk, int32_t* num_dets,
                                float* boxes, float* scores, int32_t* classes, hipStream_t st) {
   hipLaunchKernelGGL(end2end_pack, dim3(B), dim3(NT), 0, st, det, count, B, max_det, topk, num_dets, boxes, scores,
@@ -424,9 +529,9 @@ size_t nms_workspace_bytes(int B, int N, int no, int multi, int max_nms) {
   return layout(B, N, no - 5, multi, max_nms).total;
 }
 
-hipError_t launch_nms(const float* z, int B, int N, int no, float conf, float iou, int multi, int agnostic,
-                      int per_class, const int32_t* classes, int ncls, int max_det, int max_nms, float* det,
-                      int64_t* src_row, int32_t* count, void* ws, hipStream_t st) {
+hipError_t launch_nms(const float* z, const void* rowbest, int B, int N, int no, float conf, float iou, int multi,
+                      int agnostic, int per_class, const int32_t* classes, int ncls, int max_det, int max_nms,
+                      float* det, int64_t* src_row, int32_t* count, void* ws, hipStream_t st) {
   const Layout L = layout(B, N, no - 5, multi, max_nms);
   unsigned char* w = reinterpret_cast<unsigned char*>(ws);
   NmsArgs a;
@@ -462,9 +567,12 @@ hipError_t launch_nms(const float* z, int B, int N, int no, float conf, float io
   hipError_t e;
   if ((e = hipMemsetAsync(det, 0, sizeof(float) * 6 * (size_t)B * max_det, st)) != hipSuccess) return e;
   if ((e = hipMemsetAsync(src_row, 0xff, sizeof(int64_t) * (size_t)B * max_det, st)) != hipSuccess) return e;
-  int gx = (N + 4 * 8 - 1) / (4 * 8);  // 4 waves per block, ~8 rows per wave
+  int gx = (N + NT - 1) / NT;   // a lane per row
   if (gx > 1024) gx = 1024;
-  hipLaunchKernelGGL(nms_rows, dim3(gx, B), dim3(NT), 0, st, a);
+  if (rowbest && !a.multi && !classes)
+    hipLaunchKernelGGL(nms_rows_from_best, dim3(gx, B), dim3(NT), 0, st, a, reinterpret_cast<const RowBest*>(rowbest));
+  else
+    hipLaunchKernelGGL(nms_rows, dim3(gx, B), dim3(NT), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;
   hipLaunchKernelGGL(nms_scan, dim3(B), dim3(SORT_T), 0, st, a);
   if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -17,9 +17,10 @@
 
 namespace yv7 {
 size_t nms_workspace_bytes(int B, int N, int no, int multi, int max_nms);
-hipError_t launch_nms(const float* z, int B, int N, int no, float conf, float iou, int multi, int agnostic,
-                      int per_class, const int32_t* classes, int ncls, int max_det, int max_nms, float* det,
-                      int64_t* src_row, int32_t* count, void* ws, hipStream_t st);
+hipError_t launch_nms(const float* z, const void* rowbest, int B, int N, int no, float conf, float iou, int multi,
+                      int agnostic, int per_class, const int32_t* classes, int ncls, int max_det, int max_nms,
+                      float* det, int64_t* src_row, int32_t* count, void* ws, hipStream_t st);
+hipError_t launch_row_best(const float* z, int B, int N, int no, void* rowbest, hipStream_t st);
 hipError_t launch_end2end_pack(const float* det, const int32_t* count, int B, int max_det, int topk,
                                int32_t* num_dets, float* boxes, float* scores, int32_t* classes, hipStream_t st);
 }  // namespace yv7
@@ -270,8 +271,8 @@ int yv7_tensor_info(const yv7_plan* p, int id, int B, int H, int W, int64_t* off
   return 0;
 }
 
-int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, float* z, float* raw, void* ws,
-                size_t ws_bytes, void* stream) {
+int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, float* z, float* raw,
+                yv7_row_best* rowbest, void* ws, size_t ws_bytes, void* stream) {
   if (!p || !x || !z || !ws) return fail(YV7_E_ARG, "yv7_forward: null argument");
   if (x_dtype != YV7_DT_F32 && x_dtype != YV7_DT_F16) return fail(YV7_E_ARG, "yv7_forward: bad x_dtype");
   if (int rc = check_hw(p, B, H, W)) return rc;
@@ -311,6 +312,9 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
       racc += (size_t)B * lvl_rows[l] * p->no;
     }
   }
+  // fp16 plans score the rows in the head's epilogue; other paths derive the records from z after the
+  // last op
+  const bool rowbest_fused = rowbest && yv7::det_writes_rowbest(p->dtype);
   hipEvent_t* ev = nullptr;
   if (p->prof_used < p->prof_max) {
     ev = &p->events[(size_t)p->prof_used * (p->ops.size() + 1)];
@@ -369,6 +373,7 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
           c.no = p->no;
           c.stride = p->stride[o.level];
           for (int a = 0; a < p->na * 2; ++a) c.anchor[a] = p->anchor_grid[o.level * p->na * 2 + a];
+          c.best = rowbest_fused ? reinterpret_cast<float*>(rowbest) : nullptr;
           e = yv7::launch_conv(p->dtype, c, true, st);
         }
         break;
@@ -430,6 +435,9 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
     if (e != hipSuccess) return hip_fail(e, "yv7_forward launch");
     if (ev && (e = hipEventRecord(ev[i + 1], st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
+  if (rowbest && !rowbest_fused &&
+      (e = yv7::launch_row_best(z, B, nrows, p->no, rowbest, st)) != hipSuccess)
+    return hip_fail(e, "yv7_forward row scores");
   return 0;
 }
 
@@ -447,12 +455,12 @@ static int nms_check(const float* z, int B, int N, int no, int max_det, int max_
   return 0;
 }
 
-int yv7_nms(const float* z, int B, int N, int no, float conf_thres, float iou_thres, int multi_label, int agnostic,
-            const int32_t* classes, int ncls, int max_det, int max_nms, float* det, int64_t* src_row, int32_t* count,
-            void* ws, size_t ws_bytes, void* stream) {
+int yv7_nms(const float* z, const yv7_row_best* rowbest, int B, int N, int no, float conf_thres, float iou_thres,
+            int multi_label, int agnostic, const int32_t* classes, int ncls, int max_det, int max_nms, float* det,
+            int64_t* src_row, int32_t* count, void* ws, size_t ws_bytes, void* stream) {
   if (int rc = nms_check(z, B, N, no, max_det, max_nms, ws, ws_bytes, multi_label)) return rc;
   if (!det || !src_row || !count || (ncls > 0 && !classes)) return fail(YV7_E_ARG, "yv7_nms: null output");
-  hipError_t e = yv7::launch_nms(z, B, N, no, conf_thres, iou_thres, multi_label, agnostic, 0,
+  hipError_t e = yv7::launch_nms(z, rowbest, B, N, no, conf_thres, iou_thres, multi_label, agnostic, 0,
                                  ncls > 0 ? classes : nullptr, ncls, max_det, max_nms, det, src_row, count, ws,
                                  reinterpret_cast<hipStream_t>(stream));
   if (e != hipSuccess) return hip_fail(e, "yv7_nms");
@@ -490,8 +498,8 @@ int yv7_end2end(const float* z, int B, int N, int no, float conf_thres, float io
   int64_t* src = reinterpret_cast<int64_t*>(w + src_off);
   int32_t* cnt = reinterpret_cast<int32_t*>(w + cnt_off);
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
-  hipError_t e = yv7::launch_nms(z, B, N, no, conf_thres, iou_thres, 1, 0, 1, nullptr, 0, topk, max_nms, det, src,
-                                 cnt, ws, st);
+  hipError_t e = yv7::launch_nms(z, nullptr, B, N, no, conf_thres, iou_thres, 1, 0, 1, nullptr, 0, topk, max_nms,
+                                 det, src, cnt, ws, st);
   if (e != hipSuccess) return hip_fail(e, "yv7_end2end nms");
   e = yv7::launch_end2end_pack(det, cnt, B, topk, topk, num_dets, det_boxes, det_scores, det_classes, st);
   if (e != hipSuccess) return hip_fail(e, "yv7_end2end pack");

@@ -67,6 +67,7 @@ struct ConvParams {
   // Detect epilogue
   float* z;           // [B, N, no] fp32
   float* raw;         // [B, na, Ho, Wo, no] fp32 for this level (nullable)
+  float* best;        // [B, N] yv7_row_best records (nullable; written by the fp16 head epilogue)
   int nrows, row_off, na, no;
   float stride, anchor[8];  // anchor[2*a + {0,1}] pixels
   int variant;        // 0 = tuned dispatch; >0 forces a kernel variant (microbenchmarks / A-B tests)
@@ -85,6 +86,7 @@ struct StemParams {
 
 // Host launchers (defined in the .hip files, called from the runtime).
 hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t st);
+bool det_writes_rowbest(int dtype);   // true when the head kernel launch_conv picks fills ConvParams::best
 hipError_t launch_conv_f16(const ConvParams& p, bool detect, hipStream_t st);
 bool halo_supported(const ConvParams& p);
 hipError_t launch_conv_halo(const ConvParams& p, hipStream_t st);

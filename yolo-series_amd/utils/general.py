@@ -98,10 +98,16 @@ _WS = _NmsWorkspace()
 
 
 def nms_batched(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnostic=False, multi_label=False,
-                max_det=MAX_DET, max_nms=MAX_NMS, out=None):
-    """Stream-ordered batched NMS: returns device tensors (det [B,max_det,6], src_row [B,max_det], count [B])."""
+                max_det=MAX_DET, max_nms=MAX_NMS, out=None, rowbest=None):
+    """Stream-ordered batched NMS: returns device tensors (det [B,max_det,6], src_row [B,max_det], count [B]).
+
+    rowbest: the forward's per-row score records (Plan.forward_into(..., rowbest=)); found automatically
+    for a z returned by Model.forward / Plan.forward that has not been modified since."""
     if not prediction.is_cuda:
         raise RuntimeError('non_max_suppression runs on a ROCm device (libyv7); got a CPU tensor')
+    if rowbest is None:
+        from yv7.runtime import row_scores
+        rowbest = row_scores.lookup(prediction)
     z = prediction.detach()
     if z.dtype != torch.float32:
         z = z.float()
@@ -125,7 +131,8 @@ def nms_batched(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnos
     ws = _WS.get(dev, nbytes)
     stream = torch.cuda.current_stream(dev).cuda_stream
     with torch.cuda.device(dev):
-        rc = L.yv7_nms(z.data_ptr(), B, N, no, float(conf_thres), float(iou_thres), multi, int(bool(agnostic)),
+        rc = L.yv7_nms(z.data_ptr(), rowbest.data_ptr() if rowbest is not None else None, B, N, no,
+                       float(conf_thres), float(iou_thres), multi, int(bool(agnostic)),
                        cls_t.data_ptr() if cls_t is not None else None, ncls, max_det, max_nms, det.data_ptr(),
                        src.data_ptr(), cnt.data_ptr(), ws.data_ptr(), ws.numel(), stream)
     _lib.check(rc, 'yv7_nms')

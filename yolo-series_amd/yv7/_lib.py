@@ -54,12 +54,12 @@ SIGNATURES = {
     'yv7_plan_destroy': (None, [_vp]),
     'yv7_workspace_bytes': (_sz, [_vp, _i, _i, _i]),
     'yv7_num_rows': (_i64, [_vp, _i, _i]),
-    'yv7_forward': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _sz, _vp]),
+    'yv7_forward': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     'yv7_profile_enable': (_i, [_vp, _i]),
     'yv7_profile_read': (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_float)]),
     'yv7_tensor_info': (_i, [_vp, _i, _i, _i, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     'yv7_nms_workspace_bytes': (_sz, [_i, _i, _i, _i, _i]),
-    'yv7_nms': (_i, [_vp, _i, _i, _i, _f, _f, _i, _i, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
+    'yv7_nms': (_i, [_vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     'yv7_end2end_workspace_bytes': (_sz, [_i, _i, _i, _i]),
     'yv7_end2end': (_i, [_vp, _i, _i, _i, _f, _f, _i, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
 }

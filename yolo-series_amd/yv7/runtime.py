@@ -8,11 +8,37 @@ and the whole network is one yv7_forward call on the current stream.
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 
 from yv7 import _lib as L
 from yv7.graph import compile_model
+
+
+class _RowScores:
+    """z tensor -> the yv7_row_best records its forward wrote (include/yv7.h), so that
+    non_max_suppression(pred) can skip re-reading every row of z.  An entry is used only for the very
+    tensor object the forward returned and only while its version counter is unchanged (any in-place
+    edit of z bumps it), so a modified z always takes the full path."""
+
+    def __init__(self):
+        self._m = {}
+
+    def attach(self, z, rowbest):
+        for k in [k for k, (ref, _, _) in self._m.items() if ref() is None]:
+            del self._m[k]
+        self._m[id(z)] = (weakref.ref(z), z._version, rowbest)
+
+    def lookup(self, z):
+        e = self._m.get(id(z))
+        if e is None:
+            return None
+        ref, ver, rowbest = e
+        return rowbest if ref() is z and z._version == ver else None
+
+
+row_scores = _RowScores()
 
 
 class Plan:
@@ -149,7 +175,8 @@ class Plan:
                 out.append((kind, 0.0, 2 * B * Hi * Wi * c * es))
         return out
 
-    def forward_into(self, x, z, raw=None, stream=None):
+    def forward_into(self, x, z, raw=None, stream=None, rowbest=None):
+        """Forward into caller buffers; rowbest (optional): [B, N, 4] 32-bit yv7_row_best records."""
         B, C, H, W = x.shape
         if C != 3:
             raise ValueError(f'expected a [B,3,H,W] image batch, got {tuple(x.shape)}')
@@ -161,7 +188,9 @@ class Plan:
         if stream is None:
             stream = torch.cuda.current_stream(self.device).cuda_stream
         rc = L.lib().yv7_forward(self._h, x.data_ptr(), xdt, B, H, W, z.data_ptr(),
-                                 raw.data_ptr() if raw is not None else None, ws.data_ptr(), ws.numel(), stream)
+                                 raw.data_ptr() if raw is not None else None,
+                                 rowbest.data_ptr() if rowbest is not None else None, ws.data_ptr(), ws.numel(),
+                                 stream)
         L.check(rc, 'yv7_forward')
 
     def forward(self, x, want_raw=True):
@@ -174,7 +203,9 @@ class Plan:
             L.check(-2, f'yv7_num_rows(H={H}, W={W})')
         z = torch.empty((B, N, self.no), dtype=torch.float32, device=x.device)
         raw = torch.empty((B * N * self.no,), dtype=torch.float32, device=x.device) if want_raw else None
-        self.forward_into(x, z, raw)
+        rowbest = torch.empty((B, N, 4), dtype=torch.float32, device=x.device)
+        self.forward_into(x, z, raw, rowbest=rowbest)
+        row_scores.attach(z, rowbest)
         xs = None
         if want_raw:
             xs, o = [], 0
