@@ -188,40 +188,60 @@ __global__ __launch_bounds__(NT) void row_best_kernel(const float* __restrict__ 
   }
 }
 
-// Stage 2: per-image exclusive scan (one workgroup of SORT_T threads per image).
+// Stage 2: per-image exclusive scan (one workgroup of SORT_T threads per image): each thread scans a
+// contiguous run of rows serially, one workgroup-wide scan joins the runs — a single pass.
 __global__ __launch_bounds__(SORT_T) void nms_scan(const NmsArgs a) {
   const int b = blockIdx.x;
   __shared__ int wsum[SORT_T / 64];
-  __shared__ int carry;
-  if (threadIdx.x == 0) carry = 0;
-  __syncthreads();
   const int* cnt = a.cnt + (size_t)b * a.N;
   int* offs = a.offs + (size_t)b * a.N;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int base = 0; base < a.N; base += SORT_T) {
-    const int i = base + threadIdx.x;
-    const int v = i < a.N ? cnt[i] : 0;
-    int s = v;  // inclusive wave scan
-    for (int off = 1; off < 64; off <<= 1) {
-      const int t = __shfl_up(s, off);
-      if (lane >= off) s += t;
-    }
-    if (lane == 63) wsum[wv] = s;
-    __syncthreads();
-    int pre = carry;
-    for (int k = 0; k < wv; ++k) pre += wsum[k];
-    if (i < a.N) offs[i] = pre + s - v;
-    __syncthreads();
-    if (threadIdx.x == SORT_T - 1) carry = pre + s;
-    __syncthreads();
+  const int per = (a.N + SORT_T - 1) / SORT_T;
+  const int r0 = threadIdx.x * per, r1 = r0 + per < a.N ? r0 + per : a.N;
+  int tot = 0;
+  for (int r = r0; r < r1; ++r) tot += cnt[r];
+  int s = tot;  // inclusive wave scan of the run totals
+  for (int off = 1; off < 64; off <<= 1) {
+    const int t = __shfl_up(s, off);
+    if (lane >= off) s += t;
   }
-  if (threadIdx.x == 0) a.ncand[b] = carry;
+  if (lane == 63) wsum[wv] = s;
+  __syncthreads();
+  int pre = 0;
+  for (int k = 0; k < wv; ++k) pre += wsum[k];
+  int run = pre + s - tot;
+  for (int r = r0; r < r1; ++r) {
+    const int v = cnt[r];
+    offs[r] = run;
+    run += v;
+  }
+  if (threadIdx.x == SORT_T - 1) a.ncand[b] = pre + s;
 }
 
-// Stage 3: write candidate records in reference order.
+// Stage 3: write candidate records in reference order.  Single-label: a lane per row; multi-label:
+// a wave per row (its classes across lanes).
 __global__ __launch_bounds__(NT) void nms_write(const NmsArgs a) {
   const int b = blockIdx.y;
   const int lane = threadIdx.x & 63;
+  if (!a.multi) {
+    for (int row = blockIdx.x * NT + threadIdx.x; row < a.N; row += gridDim.x * NT) {
+      const size_t ri = (size_t)b * a.N + row;
+      if (a.cnt[ri] == 0) continue;
+      const float* zr = a.z + ri * a.no;
+      const float cx = zr[0], cy = zr[1], w = zr[2], h = zr[3];
+      Cand c;
+      c.x1 = cx - w / 2.0f;  // xywh2xyxy (general.py:275-282)
+      c.y1 = cy - h / 2.0f;
+      c.x2 = cx + w / 2.0f;
+      c.y2 = cy + h / 2.0f;
+      c.conf = a.bconf[ri];
+      c.cls = a.bcls[ri];
+      c.row = row;
+      c.pad = 0;
+      a.cand[(size_t)b * a.cap + a.offs[ri]] = c;
+    }
+    return;
+  }
   const int wave = (blockIdx.x * NT + threadIdx.x) >> 6;
   const int nwaves = (gridDim.x * NT) >> 6;
   for (int row = wave; row < a.N; row += nwaves) {
@@ -238,13 +258,7 @@ __global__ __launch_bounds__(NT) void nms_write(const NmsArgs a) {
     c.row = row;
     c.pad = 0;
     Cand* out = a.cand + (size_t)b * a.cap + a.offs[ri];
-    if (!a.multi) {
-      if (lane == 0) {
-        c.conf = a.bconf[ri];
-        c.cls = a.bcls[ri];
-        out[0] = c;
-      }
-    } else {
+    {
       const float obj = zr[4];
       const int c0 = lane, c1 = lane + 64;
       float v0 = -1.f, v1 = -1.f;
@@ -280,18 +294,8 @@ __device__ __forceinline__ uint64_t sort_key(float conf, int idx) {
 }
 
 // Stage 4: per-image sort -> order[] of the first min(n, max_nms) candidates.
-__global__ __launch_bounds__(SORT_T) void nms_sort(const NmsArgs a) {
-  const int b = blockIdx.x;
-  const int n = a.ncand[b];
-  const Cand* cand = a.cand + (size_t)b * a.cap;
-  int* order = a.order + (size_t)b * a.max_nms;
-  const int keep = n < a.max_nms ? n : a.max_nms;
-  if (n == 0) return;
-  int P = 1;
-  while (P < n) P <<= 1;
-  extern __shared__ __attribute__((aligned(16))) uint64_t skeys[];
-  const bool in_lds = P <= LDS_SORT_MAX;
-  uint64_t* keys = in_lds ? skeys : a.keys + (size_t)b * a.pcap;
+template <typename K>
+__device__ __forceinline__ void bitonic_sort(K* keys, const Cand* cand, int n, int P, int* order, int keep) {
   for (int i = threadIdx.x; i < P; i += SORT_T) keys[i] = i < n ? sort_key(cand[i].conf, i) : ~0ull;
   __syncthreads();
   for (int k = 2; k <= P; k <<= 1) {
@@ -311,6 +315,24 @@ __global__ __launch_bounds__(SORT_T) void nms_sort(const NmsArgs a) {
     }
   }
   for (int i = threadIdx.x; i < keep; i += SORT_T) order[i] = (int)(uint32_t)keys[i];
+}
+
+__global__ __launch_bounds__(SORT_T) void nms_sort(const NmsArgs a) {
+  const int b = blockIdx.x;
+  const int n = a.ncand[b];
+  const Cand* cand = a.cand + (size_t)b * a.cap;
+  int* order = a.order + (size_t)b * a.max_nms;
+  const int keep = n < a.max_nms ? n : a.max_nms;
+  if (n == 0) return;
+  int P = 1;
+  while (P < n) P <<= 1;
+  extern __shared__ __attribute__((aligned(16))) uint64_t skeys[];
+  // two instantiations of the network: a pointer that may be LDS or global would compile to flat
+  // accesses (vector-memory latency on every LDS step)
+  if (P <= LDS_SORT_MAX)
+    bitonic_sort(skeys, cand, n, P, order, keep);
+  else
+    bitonic_sort(a.keys + (size_t)b * a.pcap, cand, n, P, order, keep);
 }
 
 __device__ __forceinline__ bool iou_gt(const float4 bi, float ai, const float4 bj, float aj, float thr) {
