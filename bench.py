@@ -8,9 +8,9 @@ Weights: seeded synthetic yolov7 weights (no checkpoints offline), packed once o
 RCCL-broadcast.  N > 1 is launched by torch.distributed.run, one process per GPU; per-GPU work is
 fixed (weak scaling); value = all images processed / max-over-ranks wall time of the K timed steps.
 
-roofline: the dominant kernel is the implicit-GEMM conv (89 launches per forward, ~90 % of GPU time).
-Its per-launch time is measured live with HIP events recorded by libyv7 around every op of every
-timed forward (on the forward's own stream); achieved = algorithmic HBM bytes per conv launch
+roofline: the dominant kernel is the implicit-GEMM conv (CONV/DETECT launches, ~90 % of GPU time).
+Its per-launch time is measured live with HIP events recorded by libyv7 around every op of the first
+two timed forwards (on the forward's own stream); achieved = algorithmic HBM bytes per conv launch
 (layer-boundary model) / mean conv launch time, against 8 TB/s.
 cpu_baseline: the oracle (CPU restatement of the reference detect.py path: torch CPU fp32 NCHW +
 restated NMS), rank 0 only, on a bounded sample of the same workload.
@@ -44,6 +44,9 @@ def parse():
     ap.add_argument('--dtype', default='f16', choices=['f16', 'f32'])
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='bounded CPU-baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
+    ap.add_argument('--no-live-events', action='store_true', help='diagnostic: time the steps without per-op HIP events')
+    ap.add_argument('--graph', action='store_true', help='replay the step as a HIP graph (measured: same speed '
+                    'as eager launches on MI355X, the inter-kernel gaps are dependency drains, not launch cost)')
     return ap.parse_args()
 
 
@@ -120,13 +123,33 @@ def main():
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
-    plan.profile_enable(a.steps)
+    # --graph: the step (~100 kernels: forward, NMS, all-gather) replayed as one captured HIP graph.
+    # The first n_live timed steps run eagerly with per-op HIP events (libyv7 profile mode, on the
+    # forward's own stream): they give the per-launch averages for the roofline without event packets
+    # between the kernels of every step.
+    graph = None
+    if a.graph:
+        graph = torch.cuda.CUDAGraph()
+        side = torch.cuda.Stream(dev)
+        side.wait_stream(torch.cuda.current_stream(dev))
+        with torch.cuda.stream(side):
+            step()
+        torch.cuda.current_stream(dev).wait_stream(side)
+        with torch.cuda.graph(graph):
+            step()
+        graph.replay()
+        torch.cuda.synchronize()
+    n_live = 0 if a.no_live_events else min(a.steps, 2)
+    plan.profile_enable(n_live)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        step()
+    for i in range(a.steps):
+        if graph is None or i < n_live:
+            step()
+        else:
+            graph.replay()
     torch.cuda.synchronize()
     if distributed:
         dist.barrier()
@@ -149,7 +172,7 @@ def main():
             conv_bytes += by
             conv_flops += fl
             nconv += 1
-    mean_launch_s = conv_ms / 1e3 / nconv
+    mean_launch_s = max(conv_ms / 1e3 / nconv, 1e-12)   # 0 only under --no-live-events
     achieved_gbs = (conv_bytes / nconv) / mean_launch_s / 1e9
     achieved_tf = (conv_flops / nconv) / mean_launch_s / 1e12
     count_mean = float(cnt.float().mean().item())
@@ -183,7 +206,7 @@ def main():
                          'mfma_frac': round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4)},
             'detail': {'forward_ms_events': round(fwd_ms, 3), 'conv_ms_events': round(conv_ms, 3),
                        'mean_dets_per_image': round(count_mean, 1), 'rows_per_image': N,
-                       'profiled_forwards': nf},
+                       'profiled_forwards': nf, 'hip_graph': graph is not None},
         }
         if not a.no_cpu_baseline and world == 1:
             res['cpu_baseline'] = cpu_baseline(a.model, a.img, a.cpu_seconds)
