@@ -30,6 +30,9 @@ import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+# HBM bytes per conv launch from PMC counters of this same workload (scripts/pmc_traffic.sh: separate
+# FETCH_SIZE / WRITE_SIZE rocprofv3 passes; scripts/pmc_traffic.py: x2 FETCH correction for gfx950)
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r1_pmc_traffic.json')
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA
 
 
@@ -176,6 +179,10 @@ def main():
     achieved_gbs = (conv_bytes / nconv) / mean_launch_s / 1e9
     achieved_tf = (conv_flops / nconv) / mean_launch_s / 1e12
     count_mean = float(cnt.float().mean().item())
+    traffic = None
+    if a.model == 'yolov7' and B == 32 and H == 640 and a.dtype == 'f16' and os.path.exists(PMC_TRAFFIC):
+        with open(PMC_TRAFFIC) as f:
+            traffic = round(json.load(f)['conv_family']['hbm_bytes_per_launch'])
 
     if rank == 0:
         value = world * B * a.steps / elapsed
@@ -198,7 +205,8 @@ def main():
                        'global_batch': world * B, 'img': H, 'parallelism': f'dp{world}',
                        'weights': 'seeded synthetic, RCCL-broadcast' if distributed else 'seeded synthetic'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': round(achieved_gbs / HBM_PEAK_GBS, 4), 'traffic': None,
+                         'frac': round(achieved_gbs / HBM_PEAK_GBS, 4), 'traffic': traffic,
+                         'traffic_unit': 'bytes per launch (PMC, profiles/r1_pmc_traffic.json)',
                          'kernel': 'conv_kernel (implicit-GEMM MFMA conv, all CONV/DETECT launches)',
                          'launches_per_forward': nconv, 'mean_launch_us': round(mean_launch_s * 1e6, 2),
                          'algorithmic_bytes_per_launch': round(conv_bytes / nconv),
