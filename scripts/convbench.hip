@@ -27,24 +27,49 @@ int main(int argc, char** argv) {
   std::vector<Shape> shapes = {
     {"3x3 64->64 @320", 32, 320, 320, 64, 64, 3, 1},
     {"3x3 64->64 @160", 32, 160, 160, 64, 64, 3, 1},
+    {"3x3 64->64 @80", 32, 80, 80, 64, 64, 3, 1},
+    {"3x3 128->64 @80", 32, 80, 80, 128, 64, 3, 1},
     {"3x3 128->128 @80", 32, 80, 80, 128, 128, 3, 1},
+    {"3x3 128->128 @40", 32, 40, 40, 128, 128, 3, 1},
+    {"3x3 256->128 @40", 32, 40, 40, 256, 128, 3, 1},
     {"3x3 256->256 @40", 32, 40, 40, 256, 256, 3, 1},
+    {"3x3 256->256 @20", 32, 20, 20, 256, 256, 3, 1},
+    {"3x3 512->256 @20", 32, 20, 20, 512, 256, 3, 1},
     {"3x3 512->512 @20", 32, 20, 20, 512, 512, 3, 1},
     {"3x3s2 128->128 @160", 32, 160, 160, 128, 128, 3, 2},
+    {"3x3s2 128->128 @80", 32, 80, 80, 128, 128, 3, 2},
+    {"3x3s2 256->256 @80", 32, 80, 80, 256, 256, 3, 2},
+    {"3x3s2 256->256 @40", 32, 40, 40, 256, 256, 3, 2},
+    {"3x3s2 512->512 @40", 32, 40, 40, 512, 512, 3, 2},
     {"3x3 128->256 @80", 32, 80, 80, 128, 256, 3, 1},
+    {"3x3 256->512 @40", 32, 40, 40, 256, 512, 3, 1},
     {"3x3 512->1024 @20", 32, 20, 20, 512, 1024, 3, 1},
     {"1x1 256->256 @160", 32, 160, 160, 256, 256, 1, 1},
-    {"1x1 128->64 @160", 32, 160, 160, 128, 64, 1, 1},
-    {"1x1 512->512 @80", 32, 80, 80, 512, 512, 1, 1},
-    {"1x1 1024->1024 @40", 32, 40, 40, 1024, 1024, 1, 1},
-    {"1x1 512->256 @80", 32, 80, 80, 512, 256, 1, 1},
-    {"1x1 1024->256 @40", 32, 40, 40, 1024, 256, 1, 1},
     {"1x1 256->128 @160", 32, 160, 160, 256, 128, 1, 1},
-    {"GEMM 4096^2 K4096", 32, 32, 32, 4096, 4096, 1, 1},
+    {"1x1 128->128 @160", 32, 160, 160, 128, 128, 1, 1},
+    {"1x1 512->512 @80", 32, 80, 80, 512, 512, 1, 1},
+    {"1x1 512->256 @80", 32, 80, 80, 512, 256, 1, 1},
+    {"1x1 512->128 @80", 32, 80, 80, 512, 128, 1, 1},
+    {"1x1 256->256 @80", 32, 80, 80, 256, 256, 1, 1},
+    {"1x1 128->128 @80", 32, 80, 80, 128, 128, 1, 1},
+    {"1x1 1024->1024 @40", 32, 40, 40, 1024, 1024, 1, 1},
+    {"1x1 1024->512 @40", 32, 40, 40, 1024, 512, 1, 1},
+    {"1x1 1024->256 @40", 32, 40, 40, 1024, 256, 1, 1},
+    {"1x1 512->512 @40", 32, 40, 40, 512, 512, 1, 1},
+    {"1x1 256->256 @40", 32, 40, 40, 256, 256, 1, 1},
+    {"1x1 256->128 @40", 32, 40, 40, 256, 128, 1, 1},
+    {"1x1 128->128 @40", 32, 40, 40, 128, 128, 1, 1},
+    {"1x1 2048->512 @20", 32, 20, 20, 2048, 512, 1, 1},
+    {"1x1 1024->1024 @20", 32, 20, 20, 1024, 1024, 1, 1},
+    {"1x1 1024->512 @20", 32, 20, 20, 1024, 512, 1, 1},
+    {"1x1 512->512 @20", 32, 20, 20, 512, 512, 1, 1},
+    {"1x1 512->256 @20", 32, 20, 20, 512, 256, 1, 1},
+    {"1x1 256->256 @20", 32, 20, 20, 256, 256, 1, 1},
   };
   std::vector<int> variants;
   for (int i = 1; i < argc; ++i) variants.push_back(atoi(argv[i]));
   if (variants.empty()) variants = {0, 4, 5};
+  double tot_best = 0, tot_v0 = 0;
   size_t maxx = 0, maxy = 0, maxw = 0;
   for (auto& s : shapes) {
     maxx = std::max(maxx, yv7::bordered_pixels(s.B, s.H, s.W) * s.cin);
@@ -56,6 +81,10 @@ int main(int argc, char** argv) {
   void* zero;
   CK(hipMalloc(&x, maxx * 2)); CK(hipMalloc(&y, maxy * 2)); CK(hipMalloc(&y0, maxy * 2)); CK(hipMalloc(&w, maxw * 2));
   CK(hipMalloc(&b, 8192 * 4)); CK(hipMalloc(&zero, 4096)); CK(hipMemset(zero, 0, 4096));
+  const size_t part_bytes = (size_t)512 << 20;
+  const int cnt_n = 1 << 20;
+  float* part; int* cnt;
+  CK(hipMalloc(&part, part_bytes)); CK(hipMalloc(&cnt, cnt_n * 4)); CK(hipMemset(cnt, 0, cnt_n * 4));
   CK(hipMemset(y, 0, maxy * 2)); CK(hipMemset(y0, 0, maxy * 2));
   hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, x, maxx, 1u, 1.0f);
   CK(hipMemset(b, 0, 8192 * 4));
@@ -66,6 +95,7 @@ int main(int argc, char** argv) {
     if (filt && !strstr(s.name, filt)) continue;
     yv7::ConvParams p; memset(&p, 0, sizeof(p));
     p.x = x; p.y = y; p.w = w; p.bias = b; p.zero = zero;
+    p.part = part; p.cnt = cnt; p.part_bytes = part_bytes; p.cnt_n = cnt_n;
     p.B = s.B; p.H = s.H; p.W = s.W; p.xc = s.cin; p.xoff = 0; p.cin = s.cin;
     p.k = s.k; p.s = s.s; p.pad = s.k / 2;
     p.Ho = (s.H + 2 * p.pad - s.k) / s.s + 1; p.Wo = (s.W + 2 * p.pad - s.k) / s.s + 1;
@@ -82,10 +112,12 @@ int main(int argc, char** argv) {
     double flops = 2.0 * p.M * s.cout * p.K;
     double bytes = 2.0 * ((double)s.B * s.H * s.W * s.cin + (double)ny);
     printf("%-22s", s.name);
+    double best = 1e30; int bestv = 0;
     for (int v : variants) {
       p.variant = v;
       p.y = v == 0 ? (void*)y0 : (void*)y;
-      for (int i = 0; i < 3; ++i) CK(yv7::launch_conv(1, p, false, 0));
+      if (yv7::launch_conv(1, p, false, 0) != hipSuccess) { (void)hipGetLastError(); printf(" |%d -", v); continue; }
+      for (int i = 0; i < 2; ++i) CK(yv7::launch_conv(1, p, false, 0));
       CK(hipDeviceSynchronize());
       CK(hipEventRecord(e0, 0));
       const int it = 20;
@@ -98,11 +130,16 @@ int main(int argc, char** argv) {
         CK(hipMemcpy(hy0.data(), y0, ny * 2, hipMemcpyDeviceToHost));
         for (size_t i = 0; i < ny; ++i) maxd = std::max(maxd, (double)fabsf((float)hy[i] - (float)hy0[i]));
       }
-      printf(" | v%d %7.1f us %5.0f TF %4.2f TB/s", v, ms * 1e3, flops / ms / 1e9, bytes / ms / 1e9);
-      if (v != 0) printf(" d=%.3g", maxd);
+      printf(" |%d %6.1f %4.0fT", v, ms * 1e3, flops / ms / 1e9);
+      if (v != 0 && maxd > 0.02) printf(" d=%.3g", maxd);
+      if (v == 0) tot_v0 += ms * 1e3;
+      best = std::min(best, (double)ms * 1e3);
+      if (ms * 1e3 <= best) bestv = v;
     }
-    printf("\n");
+    printf("  best v%d\n", bestv);
+    tot_best += best;
     fflush(stdout);
   }
+  printf("total v0 %.1f us, best-of %.1f us\n", tot_v0, tot_best);
   return 0;
 }

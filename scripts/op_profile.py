@@ -9,6 +9,7 @@ from yv7.synthetic import synthetic_state_dict
 from yv7 import _lib as L
 ap = argparse.ArgumentParser(); ap.add_argument('--model', default='yolov7'); ap.add_argument('--b', type=int, default=32)
 ap.add_argument('--img', type=int, default=640); ap.add_argument('--dtype', default='f16'); ap.add_argument('--iters', type=int, default=10)
+ap.add_argument('--csv', default=''); ap.add_argument('--top', type=int, default=40)
 a = ap.parse_args()
 dt = torch.float16 if a.dtype == 'f16' else torch.float32
 m = Model(a.model); synthetic_state_dict(m, seed=0); m = m.float().fuse().eval()
@@ -37,11 +38,18 @@ for i, ((kind, fl, by), t, o) in enumerate(zip(costs, ms, plan.graph.ops)):
     tmin = max(by / 8e12, fl / 2.5e15) * 1e3
     rows.append((t, i, desc, tf, gb, tmin))
 print(f'forward {tot:.3f} ms over {n} forwards; sum of roofline minima {sum(r[5] for r in rows):.3f} ms')
-for t, i, desc, tf, gb, tmin in sorted(rows, reverse=True)[:40]:
+import csv
+if a.csv:
+    with open(a.csv, 'w') as f:
+        wr = csv.writer(f); wr.writerow(['op', 'desc', 'us', 'tflops', 'gbs', 'roof_us'])
+        for t, i, desc, tf, gb, tmin in sorted(rows, key=lambda r: r[1]):
+            wr.writerow([i, desc, round(t * 1e3, 2), round(tf, 1), round(gb, 1), round(tmin * 1e3, 2)])
+for t, i, desc, tf, gb, tmin in sorted(rows, reverse=True)[:a.top]:
     print(f'{i:3d} {desc:32s} {t*1e3:8.1f} us  {tf:7.1f} TF/s  {gb:7.1f} GB/s  roof {tmin*1e3:7.1f} us  frac {tmin/t:5.2f}')
 by_kind = {}
 for t, i, desc, tf, gb, tmin in rows:
-    k = desc.split()[0] + (' k' + desc.split()[2][1] if desc.startswith('CONV') else '')
+    o = plan.graph.ops[i]
+    k = desc.split()[0] + (f" k{o.get('k', 1)}s{o.get('s', 1)}" if desc.startswith('CONV') else '')
     by_kind.setdefault(k, [0, 0, 0]); by_kind[k][0] += t; by_kind[k][1] += tmin; by_kind[k][2] += 1
 for k, (t, tm, c) in sorted(by_kind.items(), key=lambda kv: -kv[1][0]):
     print(f'{k:10s} n={c:3d} {t:7.3f} ms roof {tm:7.3f} ms frac {tm/t:5.2f}')

@@ -93,11 +93,11 @@ struct AWalk {
   KCursor ln;         // per-lane cursor (k = kt*64 + chunk*8), non-uniform case only
   bool uni;
   int c16;
-  __device__ __forceinline__ void init(const ConvParams& p, int chunk) {
+  __device__ __forceinline__ void init(const ConvParams& p, int chunk, int kt0 = 0) {
     uni = ONE || (p.cin & 63) == 0;
     c16 = chunk * 16;
-    su.init(p, 0);
-    if (!uni) ln.init(p, chunk * 8);
+    su.init(p, kt0 * BKE);
+    if (!uni) ln.init(p, kt0 * BKE + chunk * 8);
   }
   // voffset / soffset of row j for step kt (call step() once per K step, in order)
   template <typename F>
@@ -127,6 +127,238 @@ struct AWalk {
   }
 };
 
+
+// ---------------------------------------------------------------------------------------------
+// Fused Detect epilogue (models/yolo.py:52-57, IDetect.fuseforward yolo.py:140-176) shared by the
+// tile and ring kernels.  BN >= na*no covers every head channel of BM consecutive pixels.
+// LDS: zs = the tile's z values in z's own layout, [na][BM][no] fp32 (so z leaves as straight 16-byte
+// copies), then a per-pixel table {z row of anchor 0 (int64, -1 past M), grid x, grid y} and the
+// level's pixel anchors.
+constexpr int det_tab(int BM, int BN) { return BM * BN * 4; }
+constexpr int det_lds(int BM, int BN) { return det_tab(BM, BN) + BM * 16 + 64; }
+
+__device__ __forceinline__ float det_sig(float v) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
+}
+
+struct DetTab {
+  long long* zrow0;
+  float *gx, *gy, *anc;
+};
+
+template <int BM, int BN>
+__device__ __forceinline__ DetTab det_tab_ptrs(unsigned char* smem) {
+  unsigned char* tab = smem + det_tab(BM, BN);
+  DetTab t;
+  t.zrow0 = reinterpret_cast<long long*>(tab);
+  t.gx = reinterpret_cast<float*>(tab + BM * 8);
+  t.gy = t.gx + BM;
+  t.anc = t.gy + BM;
+  return t;
+}
+
+// Step 0 (every thread; the caller then syncs): the per-pixel table.
+template <int BM, int BN, int NTH>
+__device__ __forceinline__ void det_table(const ConvParams& p, unsigned char* smem, int m0, int tid) {
+  const DetTab t = det_tab_ptrs<BM, BN>(smem);
+  const int hw = p.Ho * p.Wo;
+  for (int r = tid; r < BM; r += NTH) {
+    const int m = m0 + r;
+    const int mm = m < p.M ? m : p.M - 1;
+    const int b = mm / hw, cell = mm - b * hw;
+    const int gy = cell / p.Wo, gx = cell - gy * p.Wo;
+    t.zrow0[r] = m < p.M ? (long long)b * p.nrows + p.row_off + cell : -1;
+    t.gx[r] = (float)gx;
+    t.gy[r] = (float)gy;
+  }
+  if (tid < 8) t.anc[tid] = p.anchor[tid];
+}
+
+// Step 1 (registers): sigmoid of every logit, the Detect decode for the 4 box columns in the
+// reference's op order (xy = (s*2 - 0.5 + grid)*stride, wh = (s*2)^2 * anchor_px), into zs; the raw
+// logits (xs, optional) leave straight from the accumulators.  acc[j][i][e] = channel
+// wn*WTN + j*16 + g*4 + e of pixel m0 + wm*WTM + i*16 + li.  NOC / NAC: compile-time no / na (0 =
+// read p.no / p.na).  Branch-free per value: only the one 16-column block per wave that holds a box
+// column runs the decode (a wave-uniform test), the padding column past na*no lands on a dummy slot.
+template <int BM, int BN, int TN, int TM, int NOC, int NAC>
+__device__ __forceinline__ void det_stage(const ConvParams& p, unsigned char* smem, const f4 (&acc)[TN][TM], int m0,
+                                          int wm, int wn, int g, int li) {
+  constexpr int WTM = TM * 16, WTN = TN * 16;
+  const DetTab t = det_tab_ptrs<BM, BN>(smem);
+  float* zs = reinterpret_cast<float*>(smem);
+  const int NO = NOC ? NOC : p.no, NA = NAC ? NAC : p.na;
+  const int dummy = NA * BM * NO;   // one spare float inside BM*BN (BN > na*no)
+  const int wnu = __builtin_amdgcn_readfirstlane(wn);
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int cb = wnu * WTN + j * 16;
+    bool dec = false;
+    for (int a = 0; a < NA; ++a) dec |= cb < a * NO + 4 && cb + 16 > a * NO;
+    int zoff[4], co[4];
+    bool live[4];
+    float anc_wh[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int c = cb + g * 4 + e;
+      const int ca = c / NO;
+      co[e] = c - ca * NO;
+      live[e] = ca < NA;
+      zoff[e] = live[e] ? ca * BM * NO + co[e] : dummy;
+      anc_wh[e] = dec ? t.anc[(live[e] ? 2 * ca : 0) + (co[e] == 3 ? 1 : 0)] : 0.0f;
+    }
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int row = wm * WTM + i * 16 + li;
+      const int roff = row * NO;
+      if (dec) {
+        const float gxv = t.gx[row], gyv = t.gy[row];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float s = det_sig(acc[j][i][e]);
+          const float t2 = s * 2.0f;
+          const float xy = (t2 - 0.5f + (co[e] == 0 ? gxv : gyv)) * p.stride;
+          const float wh = (t2 * t2) * anc_wh[e];
+          zs[zoff[e] + (live[e] ? roff : 0)] = co[e] < 2 ? xy : (co[e] < 4 ? wh : s);
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) zs[zoff[e] + (live[e] ? roff : 0)] = det_sig(acc[j][i][e]);
+      }
+    }
+  }
+  if (p.raw) {
+    const int hw = p.Ho * p.Wo;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WTM + i * 16 + li;
+        const int m = m0 + row;
+        if (m >= p.M) continue;
+        const int b = m / hw, cell = m - b * hw;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int c = wnu * WTN + j * 16 + g * 4 + e;
+          const int ca = c / NO, co = c - ca * NO;
+          if (ca < NA) p.raw[((size_t)(b * NA + ca) * hw + cell) * NO + co] = acc[j][i][e];
+        }
+      }
+  }
+}
+
+template <int BM, int BN, int NTH, int NOC, int NAC>
+__device__ __forceinline__ void det_tail(const ConvParams& p, unsigned char* smem, int tid);
+
+// The whole epilogue after the main loop (LDS free): table, values, scores + z.
+template <int BM, int BN, int NTH, int TN, int TM>
+__device__ __forceinline__ void det_epilogue(const ConvParams& p, unsigned char* smem, const f4 (&acc)[TN][TM], int m0,
+                                             int wm, int wn, int g, int li, int tid) {
+  det_table<BM, BN, NTH>(p, smem, m0, tid);
+  __syncthreads();
+  const bool std85 = p.no == 85 && p.na == 3;
+  if (std85) det_stage<BM, BN, TN, TM, 85, 3>(p, smem, acc, m0, wm, wn, g, li);
+  else det_stage<BM, BN, TN, TM, 0, 0>(p, smem, acc, m0, wm, wn, g, li);
+  __syncthreads();
+  if (p.variant == 93) {   // microbenchmark hook: no z / row-score stores
+    if (reinterpret_cast<float*>(smem)[tid] == 12345.0f) p.z[tid] = 1.0f;
+    return;
+  }
+  if (std85) det_tail<BM, BN, NTH, 85, 3>(p, smem, tid);
+  else det_tail<BM, BN, NTH, 0, 0>(p, smem, tid);
+}
+
+// yv7_row_best record of one (anchor, pixel) row: objectness, first-max class score obj * cls_c and
+// its class, from the same sigmoid values z receives.  Four lanes per row, each over the classes
+// c = part, part + 4, ... (first maximum per lane), merged by shuffles: the larger score wins, an
+// equal score goes to the smaller class — the first maximum (general.py:683-684).
+template <int NC>
+__device__ __forceinline__ void det_best_lane(const float* sg, int nc, int part, float& best, int& bc) {
+  const float obj = sg[4];
+  best = -1.0f;
+  bc = 0x7fffffff;
+  if constexpr (NC > 0) {
+    float v[NC / 4];
+#pragma unroll
+    for (int i = 0; i < NC / 4; ++i) v[i] = sg[5 + part + 4 * i];
+#pragma unroll
+    for (int i = 0; i < NC / 4; ++i) {
+      const float s = v[i] * obj;
+      if (s > best) { best = s; bc = part + 4 * i; }
+    }
+  } else if (nc > 1) {
+    for (int c = part; c < nc; c += 4) {
+      const float s = sg[5 + c] * obj;
+      if (s > best) { best = s; bc = c; }
+    }
+  } else if (part == 0) {
+    best = obj;
+    bc = 0;
+  }
+}
+
+// Steps 2-3 (after det_stage and a barrier): the row scores, then z as 16-byte copies.
+template <int BM, int BN, int NTH, int NOC, int NAC>
+__device__ __forceinline__ void det_tail(const ConvParams& p, unsigned char* smem, int tid) {
+  const DetTab t = det_tab_ptrs<BM, BN>(smem);
+  const float* zs = reinterpret_cast<const float*>(smem);
+  const int hw = p.Ho * p.Wo;
+  const int NO = NOC ? NOC : p.no, NA = NAC ? NAC : p.na;
+  if (p.best) {
+    const int nc = NO - 5;
+    for (int t0 = 0; t0 < BM * NA * 4; t0 += NTH) {
+      const int tt = t0 + tid;
+      const int r = tt >> 2, part = tt & 3;     // r = a * BM + pixel
+      const int pr = r % BM, a = r / BM;
+      const bool live = r < BM * NA && t.zrow0[pr] >= 0;
+      const float* sg = zs + (live ? r : 0) * NO;
+      float best;
+      int bc;
+      if (NOC == 85) det_best_lane<80>(sg, nc, part, best, bc);
+      else det_best_lane<0>(sg, nc, part, best, bc);
+#pragma unroll
+      for (int d = 1; d < 4; d <<= 1) {
+        const float ob = __shfl_xor(best, d, 64);
+        const int oc = __shfl_xor(bc, d, 64);
+        if (ob > best || (ob == best && oc < bc)) { best = ob; bc = oc; }
+      }
+      if (live && part == 0) {
+        f4 rec;
+        rec[0] = sg[4];
+        rec[1] = best;
+        rec[2] = __builtin_bit_cast(float, bc);
+        rec[3] = 0.0f;
+        *reinterpret_cast<f4*>(p.best + (size_t)(t.zrow0[pr] + (long long)a * hw) * 4) = rec;
+      }
+    }
+  }
+  // A 4-row group of one anchor (4 consecutive pixels of one image = 4 consecutive z rows) is no
+  // float4 chunks in zs and in z.  Thread t owns chunk t % no of the groups it visits; a group whose
+  // first z row is divisible by 4 (a 16-byte aligned block) leaves as 16-byte stores, any other one
+  // (image boundary, rows past M, odd level sizes) element by element.
+  constexpr int G = BM / 4;
+  static_assert(BM % 4 == 0, "4-row groups");
+  const int gpp = NTH / NO;
+  const int c = tid % NO, gg = tid / NO;
+  if (gg < gpp) {
+    for (int idx = gg; idx < NA * G; idx += gpp) {
+      const int a = idx / G, grp = idx - a * G;
+      const long long aoff = (long long)a * hw;
+      const long long z0 = t.zrow0[grp * 4];
+      const f4 v = reinterpret_cast<const f4*>(zs + (a * BM + grp * 4) * NO)[c];
+      if (z0 >= 0 && t.zrow0[grp * 4 + 3] == z0 + 3 && ((z0 + aoff) & 3) == 0) {
+        reinterpret_cast<f4*>(p.z + (size_t)(z0 + aoff) * NO)[c] = v;
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int e = 4 * c + k, rk = e / NO, ok = e - rk * NO;
+          const long long zr = t.zrow0[grp * 4 + rk];
+          if (zr >= 0) p.z[(size_t)(zr + aoff) * NO + ok] = v[k];
+        }
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int WM, bool ONE, bool DET, int PF = 1>
 __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   constexpr int WN = 4 / WM;
@@ -136,7 +368,8 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   constexpr int RB = (BN + 31) / 32;
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int CPITCH = BN * 2 + 16;
-  constexpr int EPI = BM * CPITCH + BM * 4;   // staged C tile + output row table
+  constexpr int EPI0 = BM * CPITCH + BM * 4;   // staged C tile + output row table
+  constexpr int EPI = (DET && det_lds(BM, BN) > EPI0) ? det_lds(BM, BN) : EPI0;
   constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
 
@@ -236,7 +469,8 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   u4 ra[RA], rb[RB];
   gload(0, ra, rb);
   lstore(0, ra, rb);
-  if constexpr (PF == 1) {
+  if (DET && p.variant == 91) {   // microbenchmark hook: epilogue only
+  } else if constexpr (PF == 1) {
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) gload(kt + 1, ra, rb);
@@ -265,100 +499,11 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
 
   // accumulator acc[j][i][e]: output channel n = n0 + wn*WTN + j*16 + g*4 + e, pixel m = m0 + wm*WTM + i*16 + li
   if constexpr (DET) {
-    // Detect head (models/yolo.py:52-57): stage logits + bias as fp32 [BM][BN] in LDS, then decode in
-    // z order — for every anchor, BM consecutive pixels are BM consecutive 85-float rows of z — so
-    // z (and raw) leave as fully coalesced 4-byte streams.  BN covers all na*no head channels.
-    constexpr int DPITCH = BN * 4 + 16;
-    static_assert(BM * DPITCH + BM * 16 <= LDS, "detect staging");
-    float* Ds = reinterpret_cast<float*>(smem);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = wn * WTN + j * 16 + g * 4;
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = wm * WTM + i * 16 + li;
-        f4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = acc[j][i][e];
-        *reinterpret_cast<f4*>(reinterpret_cast<unsigned char*>(Ds) + row * DPITCH + col * 4) = v;
-      }
+    if (p.variant == 90) {   // microbenchmark hook: GEMM only
+      if (acc[0][0][0] == 12345.0f) p.z[tid] = acc[TN - 1][TM - 1][3];
+      return;
     }
-    // per-pixel table: z row of anchor 0 (int64), grid x / y
-    unsigned char* tab = smem + BM * DPITCH;
-    long long* zrow0 = reinterpret_cast<long long*>(tab);
-    float* gxs = reinterpret_cast<float*>(tab + BM * 8);
-    float* gys = gxs + BM;
-    const int hw = p.Ho * p.Wo;
-    if (tid < BM) {
-      const int m = m0 + tid;
-      const int mm = m < p.M ? m : p.M - 1;
-      const int b = mm / hw, cell = mm - b * hw;
-      const int gy = cell / p.Wo, gx = cell - gy * p.Wo;
-      zrow0[tid] = m < p.M ? (long long)b * p.nrows + p.row_off + cell : -1;
-      gxs[tid] = (float)gx;
-      gys[tid] = (float)gy;
-    }
-    __syncthreads();
-    // per-row NMS scores (yv7_row_best): objectness, first-max class score obj * cls_c, class — from
-    // the same sigmoid values the z rows below receive
-    if (p.best) {
-      for (int t = tid; t < BM * p.na; t += NT) {
-        const int pr = t % BM, a = t / BM;
-        const long long zr = zrow0[pr];
-        if (zr < 0) continue;
-        const float* lg = reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(Ds) + pr * DPITCH) +
-                          a * p.no;
-        auto sig = [](float v) { return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v)); };
-        const float obj = sig(lg[4]);
-        float best = obj;
-        int bc = 0;
-        if (p.no > 6) {
-          best = sig(lg[5]) * obj;
-          for (int c = 1; c < p.no - 5; ++c) {
-            const float v = sig(lg[5 + c]) * obj;
-            if (v > best) { best = v; bc = c; }   // strict >: the first maximum wins (general.py:683-684)
-          }
-        }
-        f4 rec;
-        rec[0] = obj;
-        rec[1] = best;
-        rec[2] = __builtin_bit_cast(float, bc);
-        rec[3] = 0.0f;
-        *reinterpret_cast<f4*>(p.best + (size_t)(zr + (long long)a * hw) * 4) = rec;
-      }
-    }
-    // thread t walks e = t, t + NT, ... over the [BM][no] elements of one anchor: pr = e / no, o = e % no
-    const int NO = p.no, step_pr = NT / NO, step_o = NT - step_pr * NO;
-    for (int a = 0; a < p.na; ++a) {
-      const float aw = p.anchor[2 * a], ah = p.anchor[2 * a + 1];
-      const long long aoff = (long long)a * hw;
-      int pr = tid / NO, o = tid - pr * NO;
-      for (; pr < BM;) {
-        const long long zr = zrow0[pr];
-        if (zr >= 0) {
-          const float v = *reinterpret_cast<const float*>(reinterpret_cast<const unsigned char*>(Ds) + pr * DPITCH +
-                                                          (a * NO + o) * 4);
-          const float sg = __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
-          float out;
-          if (o < 2) {
-            out = (sg * 2.0f - 0.5f + (o == 0 ? gxs[pr] : gys[pr])) * p.stride;
-          } else if (o < 4) {
-            const float t2 = sg * 2.0f;
-            out = (t2 * t2) * (o == 2 ? aw : ah);
-          } else {
-            out = sg;
-          }
-          p.z[(size_t)(zr + aoff) * NO + o] = out;
-          if (p.raw) {
-            const long long b = (zr - p.row_off) / p.nrows, cell = (zr - p.row_off) - b * p.nrows;
-            p.raw[((size_t)(b * p.na + a) * hw + cell) * NO + o] = v;
-          }
-        }
-        o += step_o;
-        pr += step_pr;
-        if (o >= NO) { o -= NO; ++pr; }
-      }
-    }
+    det_epilogue<BM, BN, NT>(p, smem, acc, m0, wm, wn, g, li, tid);
     return;
   }
 
@@ -402,6 +547,71 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   }
 }
 
+
+// Split-K hand-off between the S blocks of one output tile (last arriver reduces).  Every block
+// publishes its fp32 partial tile ([TN*TM][NTH] float4, coalesced) to p.part, then counts itself in
+// p.cnt[tile]; the block that counts last sums the S partials in split order 0..S-1 (the result does
+// not depend on arrival order), re-arms the counter and runs the epilogue; the others exit.
+// Protocol (MI355X_MICROARCH.md, inter-workgroup visibility, write-through form): partial stores
+// and loads are sc1 (write-through, L1-bypassing; no agent release fence, whose L2 write-back of
+// every dirty line of the XCD would cost more than the split saves), every wave's vmcnt(0), a
+// barrier, then one lane's relaxed agent atomic add; the last arriver's waves load after that add
+// returned and a barrier.  Each tile's partial lines are written once and read once per launch.
+constexpr int CPOL_SC1 = 16;
+
+template <int NTH, int TN, int TM>
+__device__ __forceinline__ bool splitk_reduce(const ConvParams& p, unsigned char* smem, f4 (&acc)[TN][TM], int tile,
+                                              int ks, int S, int tid) {
+  constexpr int Q = TN * TM;
+  const auto pr = make_rsrc(p.part, 0x7fffffffu);
+  const uint32_t tbase = (uint32_t)tile * S * Q * NTH * 16;
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[j][i]), pr,
+                                             tbase + ((uint32_t)(ks * Q + j * TM + i) * NTH + tid) * 16, 0, CPOL_SC1);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  int* flag = reinterpret_cast<int*>(smem);
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(p.cnt + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int last = old == S - 1;
+    if (last) __hip_atomic_store(p.cnt + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *flag = last;
+  }
+  __syncthreads();
+  const bool last = *flag != 0;
+  __syncthreads();   // the flag word is epilogue LDS
+  if (!last) return false;
+  f4 sum[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) sum[j][i] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  for (int s = 0; s < S; ++s) {
+    if (s == ks) {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i) sum[j][i] += acc[j][i];
+    } else {
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          sum[j][i] += __builtin_bit_cast(
+              f4, __builtin_amdgcn_raw_buffer_load_b128(pr, tbase + ((uint32_t)(s * Q + j * TM + i) * NTH + tid) * 16, 0,
+                                                        CPOL_SC1));
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = sum[j][i];
+  return true;
+}
+
 // ---------------------------------------------------------------------------------------------
 // 8-wave LDS-DMA ring (wide layers).
 //  * 512 threads = 8 waves (2 per SIMD, so one wave's fragment reads hide under the other's MFMAs),
@@ -412,7 +622,7 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
 //  * counted `s_waitcnt vmcnt(PER)` keeps the next stage in flight across a raw s_barrier (never
 //    __syncthreads in the loop: its fence would drain the DMA); the stage refilled at step kt is the
 //    one every wave finished reading at step kt-1 (its MFMAs consumed those reads before the barrier).
-template <int BM, int BN, int WM, int WN, int STAGES, bool ONE>
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, bool DET = false>
 __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 1024) ? 2 : 1) void conv_f16_ring_kernel(const ConvParams p) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -422,7 +632,8 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   constexpr int PER = RA + RB;
   constexpr int STAGE = (BM + BN) * ROWB;
   constexpr int CPITCH = BN * 2 + 16;
-  constexpr int EPI = BM * CPITCH + BM * 4;
+  constexpr int EPI0 = BM * CPITCH + BM * 4;
+  constexpr int EPI = (DET && det_lds(BM, BN) > EPI0) ? det_lds(BM, BN) : EPI0;
   constexpr int LDS = (STAGES * STAGE > EPI) ? STAGES * STAGE : EPI;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
@@ -435,8 +646,13 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int q = nwg >> 3, r = nwg & 7, xcd = bid & 7, loc = bid >> 3;
   const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + loc;
+  // split-K: the S blocks of one output tile are adjacent work ids, each sums the K steps [kb, ke)
+  const int S = (!DET && p.ksplit > 1) ? p.ksplit : 1;
+  const int tile = wgid / S, ks = wgid - tile * S;
   const int nN = (p.cout + BN - 1) / BN;
-  const int m0 = (wgid / nN) * BM, n0 = (wgid % nN) * BN;
+  const int m0 = (tile / nN) * BM, n0 = (tile % nN) * BN;
+  const int nk_all = p.kpad / BKE;
+  const int kb = ks * nk_all / S, ke = (ks + 1) * nk_all / S;
 
   const auto xr = make_rsrc(p.x, p.xbytes);
   const auto wr = make_rsrc(p.w, p.wbytes);
@@ -445,7 +661,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   const int c = (lane & 7) ^ lr;       // source chunk this lane fetches
 
   AWalk<ONE, RA> aw;
-  aw.init(p, c);
+  aw.init(p, c, kb);
   {
     PixelWalk pw(p, m0 + wave * 8 + lr);
 #pragma unroll
@@ -458,22 +674,23 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
 #pragma unroll
   for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)(((n0 + (j * NW + wave) * 8 + lr) * p.kpad + c * 8) * 2);
 
-  const int nk = p.kpad / BKE;
+  const int nk = ke - kb;   // K steps of this block; local step kt is global step kb + kt
   auto issue = [&](int kt, int slot) {
     unsigned char* As = smem + slot * STAGE;
     unsigned char* Bs = As + BM * ROWB;
-    aw.step(p, kt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * 8 * ROWB, vo, so); });
+    aw.step(p, kb + kt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * 8 * ROWB, vo, so); });
 #pragma unroll
-    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * 8 * ROWB, b_off[j], (uint32_t)kt * BKE * 2);
+    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * 8 * ROWB, b_off[j], (uint32_t)(kb + kt) * BKE * 2);
   };
 
+  // accumulators start at the bias (split 0 only)
   f4 acc[TN][TM];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
     const int col = n0 + wn * WTN + j * 16 + g * 4;
     f4 bv;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
+    for (int e = 0; e < 4; ++e) bv[e] = (col + e < p.cout && ks == 0) ? p.bias[col + e] : 0.0f;
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[j][i] = bv;
   }
@@ -483,7 +700,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
     if (s0 < nk) issue(s0, s0);
 
   int slot = 0;
-  for (int kt = 0; kt < nk; ++kt) {
+  for (int kt = 0; kt < (DET && p.variant == 94 ? 0 : nk); ++kt) {
     // stage kt must have landed; the (at most STAGES-2) stages issued after it may stay in flight
     const int ahead = nk - 1 - kt;
     if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
@@ -525,6 +742,16 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
   __syncthreads();
 
+  if (S > 1 && !splitk_reduce<NTH, TN, TM>(p, smem, acc, tile, ks, S, tid)) return;
+
+  if constexpr (DET) {
+    if (p.variant == 90) {   // microbenchmark hook: GEMM only
+      if (acc[0][0][0] == 12345.0f) p.z[tid] = acc[TN - 1][TM - 1][3];
+      return;
+    }
+    det_epilogue<BM, BN, NTH>(p, smem, acc, m0, wm, wn, g, li, tid);
+    return;
+  }
   uint32_t* yrow = reinterpret_cast<uint32_t*>(smem + BM * CPITCH);
   for (int t = tid; t < BM; t += NTH) {
     const int m = m0 + t;
@@ -564,10 +791,10 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   }
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool ONE>
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, bool DET = false>
 hipError_t launch_ring(const ConvParams& p, hipStream_t st) {
   const int nM = (p.M + BM - 1) / BM, nN = (p.cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, ONE>), dim3(nM * nN), dim3(64 * WM * WN), 0, st, p);
+  hipLaunchKernelGGL((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, ONE, DET>), dim3(nM * nN), dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
 }
 
@@ -585,10 +812,105 @@ hipError_t launch_t(const ConvParams& p, hipStream_t st) {
 
 }  // namespace
 
+namespace {
+
+// Ring-kernel configurations the split-K dispatch chooses from: tile BM x BN, waves, LDS stages.
+enum RingCfg { R256x256, R256x128, R128x128s3, R128x128s2, R128x64, R256x64, NCFG };
+constexpr int cfg_bm[NCFG] = {256, 256, 128, 128, 128, 256};
+constexpr int cfg_bn[NCFG] = {256, 128, 128, 128, 64, 64};
+
+struct Choice {
+  int cfg = -1;   // ring configuration, -1 = the legacy dispatch (halo / tile kernels / old variants)
+  int S = 1;      // K splits
+};
+
+int env_variant() {
+  static const int v = [] { const char* e = getenv("YV7_CONV_F16"); return e ? atoi(e) : 0; }();
+  return v;
+}
+
+long ring_tiles(const ConvParams& p, int cfg) {
+  return (long)((p.M + cfg_bm[cfg] - 1) / cfg_bm[cfg]) * ((p.cout + cfg_bn[cfg] - 1) / cfg_bn[cfg]);
+}
+
+// variant 100 + 10 * cfg + S forces ring configuration cfg with S K-splits (microbenchmarks).
+Choice choose(const ConvParams& p, bool det) {
+  Choice c;
+  const int variant = p.variant ? p.variant : env_variant();
+  if (det || p.cout <= 32) return c;
+  const int nk = p.kpad / BKE;
+  if (variant >= 100 && variant < 100 + 10 * NCFG) {
+    c.cfg = (variant - 100) / 10;
+    c.S = variant % 10 ? variant % 10 : 1;
+  } else if (variant == 0 && !halo_supported(p)) {
+    // Low-resolution layers (scripts/convbench.hip, bs 32, us): with at most 400 tiles of 128 x 128
+    // (and for short-K 1x1 layers up to 3200) the 2-stage 128 x 128 ring (2 blocks per CU) beats the
+    // wide tiles and the register-staged tile kernel (3x3 256->128 @40 50 -> 44, s2 512->512 @40
+    // 88 -> 82, 1x1 256->256 @80 70 -> 61, 2048->512 @20 40 -> 37); the narrowest 1x1 take 128 x 64
+    // (512->256 @20 11.7 -> 10.5); deep-K 3x3 layers under one round of tiles split K in two
+    // (256->256 @20 35 -> 30, 512->256 @20 65 -> 47, s2 256->256 @40 36 -> 30; sc1 hand-off,
+    // splitk_reduce).  Wider grids keep the tuned wide tiles below.
+    const long t128 = ring_tiles(p, R128x128s2);
+    if (p.k > 1) {
+      if (t128 <= 400) c.cfg = R128x128s2;
+      if (t128 <= 256 && nk >= 36) c.S = 2;
+    } else {
+      if (t128 <= 400 || (p.K <= 256 && t128 <= 3200)) c.cfg = R128x128s2;
+      if (t128 <= 200 && p.cout <= 256) c.cfg = R128x64;
+    }
+  }
+  if (c.S > nk) c.S = nk;
+  if (c.cfg >= 0 && c.S > 1 &&
+      (double)ring_tiles(p, c.cfg) * c.S * cfg_bm[c.cfg] * cfg_bn[c.cfg] * 4 >= 2147483648.0)
+    c.S = 1;   // partial tiles are addressed with 32-bit buffer offsets
+  return c;
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+hipError_t launch_ring_s(const ConvParams& p0, bool one, int S, hipStream_t st) {
+  ConvParams p = p0;
+  p.ksplit = S;
+  const long tiles = (long)((p.M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
+  if (S > 1 && (!p.part || !p.cnt || p.part_bytes < (size_t)tiles * S * BM * BN * 4 || p.cnt_n < tiles))
+    return hipErrorInvalidValue;   // the caller sized the scratch with conv_splitk_part_bytes
+  const unsigned nblk = (unsigned)(tiles * S);
+  if (one)
+    hipLaunchKernelGGL((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, true>), dim3(nblk), dim3(64 * WM * WN), 0, st, p);
+  else
+    hipLaunchKernelGGL((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, false>), dim3(nblk), dim3(64 * WM * WN), 0, st, p);
+  return hipGetLastError();
+}
+
+hipError_t launch_choice(const ConvParams& p, const Choice& c, bool one, hipStream_t st) {
+  switch (c.cfg) {
+    case R256x256: return launch_ring_s<256, 256, 2, 4, 2>(p, one, c.S, st);
+    case R256x128: return launch_ring_s<256, 128, 4, 2, 3>(p, one, c.S, st);
+    case R128x128s3: return launch_ring_s<128, 128, 2, 2, 3>(p, one, c.S, st);
+    case R128x128s2: return launch_ring_s<128, 128, 2, 2, 2>(p, one, c.S, st);
+    case R128x64: return launch_ring_s<128, 64, 2, 2, 3>(p, one, c.S, st);
+    case R256x64: return launch_ring_s<256, 64, 4, 2, 3>(p, one, c.S, st);
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
+size_t conv_splitk_part_bytes(const ConvParams& p) {
+  const Choice c = choose(p, false);   // (choose() keeps this under 2 GiB)
+  if (c.cfg < 0 || c.S <= 1) return 0;
+  return (size_t)ring_tiles(p, c.cfg) * c.S * cfg_bm[c.cfg] * cfg_bn[c.cfg] * 4;
+}
+
+int conv_splitk_tiles(const ConvParams& p) {
+  const Choice c = choose(p, false);
+  return (c.cfg < 0 || c.S <= 1) ? 0 : (int)ring_tiles(p, c.cfg);
+}
+
 hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   const bool one = p.k == 1 && p.s == 1 && p.pad == 0;
-  static const int env_variant = [] { const char* e = getenv("YV7_CONV_F16"); return e ? atoi(e) : 0; }();
-  const int variant = p.variant ? p.variant : env_variant;
+  const Choice ch = choose(p, det);
+  if (ch.cfg >= 0) return launch_choice(p, ch, one, st);
+  const int variant = p.variant ? p.variant : env_variant();
   if (!det && p.cout > 32) {
     if ((variant == 0 || variant == 10) && halo_supported(p)) return launch_conv_halo(p, st);
     if (variant == 4) {
@@ -621,7 +943,15 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
       if (mt * ((p.cout + 127) / 128) >= 150) return launch_ring2<256, 128, 4, 2, 3>(p, one, st);
     }
   }
-  if (det) return launch_t<64, 256, 1, true, true>(p, st);
+  if (det) {
+    // Detect head: BN = 256 covers the na*no = 255 channels of a pixel
+    // (scripts/detbench.hip, bs 32, row scores on: 64 x 256 ring, 2 blocks per CU so one block's
+    // epilogue runs beside the other's main loop: 124 / 42 / 25 us at 80 / 40 / 20; 128 x 256 ring
+    // 127 / 42 / 29; register-staged 64 x 256 tile 141 / 47 / 30)
+    if (variant == 92) return launch_t<64, 256, 1, true, true>(p, st);
+    if (variant == 97) return launch_ring<128, 256, 2, 4, 3, true, true>(p, st);
+    return launch_ring<64, 256, 1, 4, 2, true, true>(p, st);
+  }
   if (variant == 2) {  // tall tiles for narrow layers
     if (p.cout <= 32) return one ? launch_t<256, 32, 4, true, false>(p, st) : launch_t<256, 32, 4, false, false>(p, st);
     if (p.cout <= 64) return one ? launch_t<256, 64, 4, true, false>(p, st) : launch_t<256, 64, 4, false, false>(p, st);

@@ -7,6 +7,7 @@
 // without the Python dispatch); no allocation, no host sync, so callers can capture it in a graph.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -91,6 +92,58 @@ int check_hw(const yv7_plan* p, int B, int H, int W) {
 }
 
 int kpad_of(const yv7_op_desc& o) { return (o.k * o.k * o.cin + 63) / 64 * 64; }
+
+// Geometry / operand fields of a CONV or DETECT op's kernel parameters (pointers into the workspace
+// are filled by the caller).
+yv7::ConvParams conv_params(const yv7_plan* p, const yv7_op_desc& o, int B, int H, int W) {
+  const auto& ti = p->tensors[o.src];
+  const size_t es = elem_size(p->dtype);
+  yv7::ConvParams c;
+  std::memset(&c, 0, sizeof(c));
+  c.B = B;
+  c.H = H >> ti.shift;
+  c.W = W >> ti.shift;
+  c.xc = ti.channels;
+  c.xoff = o.src_coff;
+  c.cin = o.cin;
+  c.Ho = (c.H + 2 * o.pad - o.k) / o.s + 1;
+  c.Wo = (c.W + 2 * o.pad - o.k) / o.s + 1;
+  c.cout = o.cout;
+  c.k = o.k;
+  c.s = o.s;
+  c.pad = o.pad;
+  c.act = o.act;
+  c.kpad = kpad_of(o);
+  c.K = o.k * o.k * o.cin;
+  c.M = B * c.Ho * c.Wo;
+  c.xbytes = (uint32_t)tensor_bytes(p, ti, B, H, W);
+  c.wbytes = (uint32_t)((size_t)((o.cout + 31) / 32 * 32) * c.kpad * es);
+  return c;
+}
+
+// Split-K scratch behind the activation tensors: fp32 partial tiles (the largest any conv of the
+// plan needs; convs run one at a time) and the per-tile arrival counters (zeroed with the workspace,
+// re-armed by the kernels).
+struct SplitScratch {
+  size_t part_off = 0, part_bytes = 0, cnt_off = 0;
+  int cnt_n = 0;
+  size_t end = 0;
+};
+
+SplitScratch split_scratch(const yv7_plan* p, int B, int H, int W, size_t tensors_end) {
+  SplitScratch s;
+  if (p->dtype == YV7_DT_F16)
+    for (const auto& o : p->ops)
+      if (o.kind == YV7_OP_CONV) {
+        const yv7::ConvParams c = conv_params(p, o, B, H, W);
+        s.part_bytes = std::max(s.part_bytes, yv7::conv_splitk_part_bytes(c));
+        s.cnt_n = std::max(s.cnt_n, yv7::conv_splitk_tiles(c));
+      }
+  s.part_off = tensors_end;
+  s.cnt_off = align256(s.part_off + s.part_bytes);
+  s.end = align256(s.cnt_off + (size_t)s.cnt_n * 4);
+  return s;
+}
 
 }  // namespace
 
@@ -243,7 +296,7 @@ size_t yv7_workspace_bytes(const yv7_plan* p, int B, int H, int W) {
   if (!p || check_hw(p, B, H, W)) return 0;
   size_t total = 0;
   tensor_offsets(p, B, H, W, &total);
-  return total;
+  return split_scratch(p, B, H, W, total).end;
 }
 
 int64_t yv7_num_rows(const yv7_plan* p, int H, int W) {
@@ -278,6 +331,8 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   if (int rc = check_hw(p, B, H, W)) return rc;
   size_t total = 0;
   const auto off = tensor_offsets(p, B, H, W, &total);
+  const SplitScratch scr = split_scratch(p, B, H, W, total);
+  total = scr.end;
   if (ws_bytes < total) return fail(YV7_E_WORKSPACE, "yv7_forward: workspace too small (need " +
                                                          std::to_string(total) + " bytes)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
@@ -291,7 +346,6 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
     p->ws_ready = ws;
     p->ws_ready_bytes = total;
   }
-  const size_t es = elem_size(p->dtype);
   const int nrows = (int)yv7_num_rows(p, H, W);
   // raw-logit and z row offsets of each level
   std::vector<int> row_off(p->nl, 0);
@@ -331,31 +385,15 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
       }
       case YV7_OP_CONV:
       case YV7_OP_DETECT: {
-        const auto& ti = p->tensors[o.src];
-        yv7::ConvParams c;
-        std::memset(&c, 0, sizeof(c));
+        yv7::ConvParams c = conv_params(p, o, B, H, W);
         c.x = wsb + off[o.src];
-        c.B = B;
-        c.H = H >> ti.shift;
-        c.W = W >> ti.shift;
-        c.xc = ti.channels;
-        c.xoff = o.src_coff;
-        c.cin = o.cin;
-        c.Ho = (c.H + 2 * o.pad - o.k) / o.s + 1;
-        c.Wo = (c.W + 2 * o.pad - o.k) / o.s + 1;
-        c.cout = o.cout;
-        c.k = o.k;
-        c.s = o.s;
-        c.pad = o.pad;
-        c.act = o.act;
-        c.kpad = kpad_of(o);
-        c.K = o.k * o.k * o.cin;
-        c.M = B * c.Ho * c.Wo;
         c.w = wb + o.w_off;
         c.bias = reinterpret_cast<const float*>(wb + o.b_off);
         c.zero = p->zero;
-        c.xbytes = (uint32_t)tensor_bytes(p, ti, B, H, W);
-        c.wbytes = (uint32_t)((size_t)((o.cout + 31) / 32 * 32) * c.kpad * es);
+        c.part = reinterpret_cast<float*>(wsb + scr.part_off);
+        c.part_bytes = scr.part_bytes;
+        c.cnt = reinterpret_cast<int*>(wsb + scr.cnt_off);
+        c.cnt_n = scr.cnt_n;
         if (o.kind == YV7_OP_CONV) {
           const auto& to = p->tensors[o.dst];
           if (c.Ho != (H >> to.shift) || c.Wo != (W >> to.shift))

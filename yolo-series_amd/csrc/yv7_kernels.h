@@ -71,7 +71,18 @@ struct ConvParams {
   int nrows, row_off, na, no;
   float stride, anchor[8];  // anchor[2*a + {0,1}] pixels
   int variant;        // 0 = tuned dispatch; >0 forces a kernel variant (microbenchmarks / A-B tests)
+  // split-K scratch (fp16 ring kernels): fp32 partial tiles and per-tile arrival counters (zeroed once,
+  // re-armed by the kernel); ksplit > 0 forces the split count (microbenchmarks), 0 = tuned choice
+  float* part;
+  int* cnt;
+  size_t part_bytes;
+  int cnt_n;
+  int ksplit;
 };
+
+// Split-K scratch the fp16 dispatch needs for one conv (0 when it does not split).
+size_t conv_splitk_part_bytes(const ConvParams& p);
+int conv_splitk_tiles(const ConvParams& p);
 
 // Fused stem: image -> conv A (3 -> 32, 3x3, stride sa) -> conv B (32 -> 64, 3x3, stride 2).
 struct StemParams {
