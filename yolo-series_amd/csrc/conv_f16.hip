@@ -842,7 +842,7 @@ Choice choose(const ConvParams& p, bool det) {
   if (variant >= 100 && variant < 100 + 10 * NCFG) {
     c.cfg = (variant - 100) / 10;
     c.S = variant % 10 ? variant % 10 : 1;
-  } else if (variant == 0 && !halo_supported(p)) {
+  } else if (variant == 0 && !halo_supported(p) && !ws64_supported(p)) {
     // Low-resolution layers (scripts/convbench.hip, bs 32, us): with at most 400 tiles of 128 x 128
     // (and for short-K 1x1 layers up to 3200) the 2-stage 128 x 128 ring (2 blocks per CU) beats the
     // wide tiles and the register-staged tile kernel (3x3 256->128 @40 50 -> 44, s2 512->512 @40
@@ -912,6 +912,12 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   if (ch.cfg >= 0) return launch_choice(p, ch, one, st);
   const int variant = p.variant ? p.variant : env_variant();
   if (!det && p.cout > 32) {
+    // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/
+    // convbench.hip, bs 32, same box: @320 423 -> 337 us, @160 95 -> 79 us vs the halo kernel; @80,
+    // 3 tiles per CU, its prologue does not amortise); 12-16 are its microbenchmark hooks
+    if (((variant == 0 && (long)p.B * (p.H / 16) * (p.W / 16) >= 2048) || (variant >= 11 && variant <= 16)) &&
+        ws64_supported(p))
+      return launch_conv_ws64(p, st);
     if ((variant == 0 || variant == 10) && halo_supported(p)) return launch_conv_halo(p, st);
     if (variant == 4) {
       if (p.cout <= 64) return launch_ring2<256, 64, 4, 2, 3>(p, one, st);

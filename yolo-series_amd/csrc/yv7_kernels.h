@@ -100,6 +100,8 @@ hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t 
 bool det_writes_rowbest(int dtype);   // true when the head kernel launch_conv picks fills ConvParams::best
 hipError_t launch_conv_f16(const ConvParams& p, bool detect, hipStream_t st);
 bool halo_supported(const ConvParams& p);
+bool ws64_supported(const ConvParams& p);
+hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st);
 hipError_t launch_conv_halo(const ConvParams& p, hipStream_t st);
 hipError_t launch_input(int dtype, const void* x, int x_dtype, void* y, int B, int H, int W, int yc,
                         bool reorg, hipStream_t st);
