@@ -791,6 +791,217 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   }
 }
 
+
+// ---------------------------------------------------------------------------------------------
+// Persistent ring (short-K layers).  Non-persistent tiles pay, per tile, the ring fill latency and
+// an LDS-staged epilogue during which nothing streams; for K = 128..512 that is most of the tile.
+// Here every block walks tiles t = blockIdx.x, + gridDim.x, ...:
+//  * the LDS-DMA ring of K steps runs on across tile boundaries — the next tile's first stages are
+//    in flight while the current tile finishes and writes back;
+//  * the epilogue goes straight from the accumulators (bias from LDS at accumulator init,
+//    compile-time activation, fp16, one v_permlane16_swap per dword so a lane holds 8 consecutive
+//    channels, 16-byte stores into the destination channel slice), so the ring never stops for
+//    LDS staging;
+//  * counted vmcnt waits: the loads younger than the awaited stage are the next stages and, right
+//    after a tile boundary, the previous tile's stores (their number is known per step).
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int ACT>
+__global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 76 * 1024) ? 2 : 1) void conv_f16_pring_kernel(
+    const ConvParams p) {
+  constexpr int NW = WM * WN, NTH = 64 * NW;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int RA = BM / 8 / NW, RB = BN / 8 / NW;
+  static_assert(RA * 8 * NW == BM && RB * 8 * NW == BN, "tile rows must split into 8-row groups per wave");
+  static_assert(TN % 2 == 0, "the epilogue pairs 16-channel groups");
+  constexpr int PER = RA + RB;
+  constexpr int NST = TM * TN / 2;   // epilogue stores per lane per tile
+  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int BIAS = 4096;         // bias vector (<= 1024 channels) behind the ring
+  __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + BIAS];
+  float* bias_l = reinterpret_cast<float*>(smem + STAGES * STAGE);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, li = lane & 15;
+  const int lr = lane >> 3, c = (lane & 7) ^ lr;
+
+  const int nN = (p.cout + BN - 1) / BN;
+  const int T = ((p.M + BM - 1) / BM) * nN;
+  const int G = gridDim.x;
+  const int nk = p.kpad / BKE;
+  const int ntl = (T - (int)blockIdx.x + G - 1) / G;
+  const int nsteps = ntl * nk;
+
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto wr = make_rsrc(p.w, p.wbytes);
+  const auto yr = make_rsrc(p.y, 0x7fffffffu);
+
+  for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
+
+  // ---- issue cursor: global step ig = (local tile it, step ikt)
+  AWalk<ONE, RA> aw;
+  uint32_t b_off[RB];
+  int ig = 0, it = 0, ikt = 0;
+  auto issue_next = [&]() {
+    if (ikt == 0) {
+      const int t = blockIdx.x + it * G;
+      const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+      aw.init(p, c, 0);
+      PixelWalk pw(p, m0 + wave * 8 + lr);
+#pragma unroll
+      for (int j = 0; j < RA; ++j) {
+        if (j) pw.advance(p, NW * 8);
+        aw.off[j] = a_origin(p, pw.b, pw.ho, pw.wo, c);
+      }
+#pragma unroll
+      for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)(((n0 + (j * NW + wave) * 8 + lr) * p.kpad + c * 8) * 2);
+    }
+    const int slot = ig % STAGES;
+    unsigned char* As = smem + slot * STAGE;
+    unsigned char* Bs = As + BM * ROWB;
+    aw.step(p, ikt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * 8 * ROWB, vo, so); });
+#pragma unroll
+    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * 8 * ROWB, b_off[j], (uint32_t)ikt * BKE * 2);
+    ++ig;
+    if (++ikt == nk) { ikt = 0; ++it; }
+  };
+
+  // ---- compute cursor
+  f4 acc[TN][TM];
+  int cm0 = 0, cn0 = 0;
+  auto init_tile = [&](int i) {
+    const int t = blockIdx.x + i * G;
+    cm0 = (t / nN) * BM;
+    cn0 = (t % nN) * BN;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = cn0 + wn * WTN + j * 16 + g * 4;
+      f4 bv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? bias_l[col + e] : 0.0f;
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) acc[j][ii] = bv;
+    }
+  };
+  const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
+  auto epilogue = [&]() {
+    PixelWalk pw(p, cm0 + wm * WTM + li);
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii) {
+      if (ii) pw.advance(p, 16);
+      const int m = cm0 + wm * WTM + ii * 16 + li;
+      const uint32_t yo = (uint32_t)((pix_index(pw.b, pw.ho, pw.wo, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
+#pragma unroll
+      for (int mp = 0; mp < TN / 2; ++mp) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        h4 va, vb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          va[e] = (_Float16)act_t<ACT>(acc[2 * mp][ii][e]);
+          vb[e] = (_Float16)act_t<ACT>(acc[2 * mp + 1][ii][e]);
+        }
+        const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+        const u4 v = {s0[0], s1[0], s0[1], s1[1]};
+        const int n = cn0 + wn * WTN + mp * 32 + (int)lane_ch;
+        // rows past M / channels past cout: an offset beyond the buffer drops the store
+        const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
+        __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+      }
+    }
+  };
+
+#pragma unroll
+  for (int s0 = 0; s0 < STAGES - 1; ++s0)
+    if (ig < nsteps) issue_next();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bias_l writes of this wave
+  __builtin_amdgcn_s_barrier();
+  init_tile(0);
+
+  int ci = 0, ckt = 0;
+  for (int gs = 0; gs < nsteps; ++gs) {
+    // stage gs has landed once at most `younger` vector-memory ops of this wave are outstanding
+    const int ndma = min(STAGES - 2, nsteps - 1 - gs);
+    const bool st = ci > 0 && ckt <= STAGES - 2;
+    const int younger = ndma * PER + (st ? NST : 0);
+    if (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (younger == PER) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else if (younger == 2 * PER) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
+    else if (younger == NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    else if (younger == PER + NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + NST) : "memory");
+    else if (younger == 2 * PER + NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER + NST) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ig < nsteps) issue_next();   // refills the slot every wave finished reading at step gs-1
+    const unsigned char* As = smem + (gs % STAGES) * STAGE;
+    const unsigned char* Bs = As + BM * ROWB;
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      const int ch = sb * 4 + g;
+      u4 xa[TM], wb[TN];
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) {
+        const int row = wm * WTM + ii * 16 + li;
+        xa[ii] = *reinterpret_cast<const u4*>(As + row * ROWB + swz(row, ch) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WTN + j * 16 + li;
+        wb[j] = *reinterpret_cast<const u4*>(Bs + row * ROWB + swz(row, ch) * 16);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int ii = 0; ii < TM; ++ii)
+          acc[j][ii] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]),
+                                                              __builtin_bit_cast(h8, xa[ii]), acc[j][ii], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+    if (++ckt == nk) {
+      epilogue();
+      ckt = 0;
+      if (++ci < ntl) init_tile(ci);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE>
+hipError_t launch_pring_act(const ConvParams& p, int grid, hipStream_t st) {
+  if (p.act == 1)
+    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 1>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  else if (p.act == 2)
+    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 2>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  else
+    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 0>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  return hipGetLastError();
+}
+
+int device_cus() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+// occ: resident blocks per CU the grid is sized for
+template <int BM, int BN, int WM, int WN, int STAGES>
+hipError_t launch_pring(const ConvParams& p, bool one, int occ, hipStream_t st) {
+  if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8) return hipErrorInvalidValue;
+  const long T = (long)((p.M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
+  const int grid = (int)(T < (long)device_cus() * occ ? T : (long)device_cus() * occ);
+  return one ? launch_pring_act<BM, BN, WM, WN, STAGES, true>(p, grid, st)
+             : launch_pring_act<BM, BN, WM, WN, STAGES, false>(p, grid, st);
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, bool DET = false>
 hipError_t launch_ring(const ConvParams& p, hipStream_t st) {
   const int nM = (p.M + BM - 1) / BM, nN = (p.cout + BN - 1) / BN;
@@ -908,9 +1119,33 @@ int conv_splitk_tiles(const ConvParams& p) {
 
 hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   const bool one = p.k == 1 && p.s == 1 && p.pad == 0;
+  const int variant = p.variant ? p.variant : env_variant();
+  if (!det && variant == 0 && p.cout > 32 && p.cout <= 1024 && p.cout % 8 == 0) {
+    // Persistent ring (scripts/convbench.hip, bs 32, same box, us): short-K 1x1 layers and the
+    // 128-channel / low-resolution 512-channel 3x3 layers, whose per-tile fill + epilogue the
+    // non-persistent kernels cannot hide.  256 x 256 tiles once every CU gets >= 6 of them
+    // (1x1 256->256 @160 304 -> 226, 512->512 @80 208 -> 183), else 128 x 128 with two blocks per
+    // CU (1x1 128->128 @160 110 -> 89, 256->128 @160 161 -> 131, 256->256 @80 61 -> 55, 3x3
+    // 128->128 @80 86 -> 81, s2 128->128 @160 96 -> 90, 512->512 @20 80 -> 76).
+    const long t256 = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
+    if (one) {
+      if (p.K >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
+      if (p.K <= 512 && p.M >= 51200) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
+    } else if (p.k == 3 && (p.cout == 128 || (p.cout == 512 && p.Ho <= 20))) {
+      return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
+    }
+  }
   const Choice ch = choose(p, det);
   if (ch.cfg >= 0) return launch_choice(p, ch, one, st);
-  const int variant = p.variant ? p.variant : env_variant();
+  if (!det && p.cout > 32) {
+    // persistent ring configurations (microbenchmarks: 201..206)
+    if (variant == 201) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
+    if (variant == 202) return launch_pring<256, 128, 4, 2, 3>(p, one, 1, st);
+    if (variant == 203) return launch_pring<128, 128, 2, 2, 3>(p, one, 1, st);
+    if (variant == 204) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
+    if (variant == 205) return launch_pring<256, 128, 4, 2, 2>(p, one, 1, st);
+    if (variant == 206) return launch_pring<128, 256, 2, 4, 2>(p, one, 1, st);
+  }
   if (!det && p.cout > 32) {
     // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/
     // convbench.hip, bs 32, same box: @320 423 -> 337 us, @160 95 -> 79 us vs the halo kernel; @80,
