@@ -18,6 +18,8 @@
  *                     torchvision.ops.nms call at general.py:704
  *   yv7_end2end       TRT EfficientNMS_TRT plugin contract    models/experimental.py:111-156,
  *                     utils/add_nms.py:94-138 (fixed-shape num_dets/boxes/scores/classes)
+ *   yv7_letterbox     letterbox() + the detect.py input         utils/datasets.py:1277-1307,
+ *                     conversion                                detect.py:100-104, datasets.py:199
  */
 #ifndef YV7_H
 #define YV7_H
@@ -153,6 +155,18 @@ size_t yv7_end2end_workspace_bytes(int B, int N, int no, int topk);
 int yv7_end2end(const float* z, int B, int N, int no, float conf_thres, float iou_thres, int topk,
                 int32_t* num_dets, float* det_boxes, float* det_scores, int32_t* det_classes,
                 void* workspace, size_t ws_bytes, void* stream);
+
+/* Frame pre-processing (replaces utils/datasets.py:1277-1307 letterbox() with its cv2.resize
+ * INTER_LINEAR + cv2.copyMakeBorder, and detect.py:100-104's BGR->RGB / HWC->CHW / half / 255):
+ * src: B uint8 frames [B][H][W][3] BGR on the device; the host computes the letterbox geometry
+ * (new_h x new_w resized image placed at (top, left) of an out_h x out_w canvas of colour
+ * (pad_b, pad_g, pad_r)), exactly as letterbox() does.  out_kind: 0 = uint8 [B][out_h][out_w][3]
+ * BGR (the letterboxed frame), 1 = fp16 [B][3][out_h][out_w] RGB / 255, 2 = fp32 likewise (the model
+ * input).  The workspace holds the resize tables (yv7_letterbox_workspace_bytes).  Asynchronous. */
+size_t yv7_letterbox_workspace_bytes(int new_h, int new_w);
+int yv7_letterbox(const void* src, int B, int H, int W, int new_h, int new_w, int top, int left, int out_h,
+                  int out_w, int pad_b, int pad_g, int pad_r, int out_kind, void* dst, void* workspace,
+                  size_t ws_bytes, void* stream);
 
 #ifdef __cplusplus
 }

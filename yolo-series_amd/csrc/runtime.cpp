@@ -22,6 +22,9 @@ hipError_t launch_nms(const float* z, const void* rowbest, int B, int N, int no,
                       int agnostic, int per_class, const int32_t* classes, int ncls, int max_det, int max_nms,
                       float* det, int64_t* src_row, int32_t* count, void* ws, hipStream_t st);
 hipError_t launch_row_best(const float* z, int B, int N, int no, void* rowbest, hipStream_t st);
+size_t letterbox_workspace_bytes(int nh, int nw);
+hipError_t launch_letterbox(const uint8_t* src, int B, int H, int W, int nh, int nw, int top, int left, int oh,
+                            int ow, const uint8_t pad[3], int out_kind, void* dst, void* ws, hipStream_t st);
 hipError_t launch_end2end_pack(const float* det, const int32_t* count, int B, int max_det, int topk,
                                int32_t* num_dets, float* boxes, float* scores, int32_t* classes, hipStream_t st);
 }  // namespace yv7
@@ -541,6 +544,30 @@ int yv7_end2end(const float* z, int B, int N, int no, float conf_thres, float io
   if (e != hipSuccess) return hip_fail(e, "yv7_end2end nms");
   e = yv7::launch_end2end_pack(det, cnt, B, topk, topk, num_dets, det_boxes, det_scores, det_classes, st);
   if (e != hipSuccess) return hip_fail(e, "yv7_end2end pack");
+  return 0;
+}
+
+size_t yv7_letterbox_workspace_bytes(int new_h, int new_w) {
+  if (new_h <= 0 || new_w <= 0) return 0;
+  return yv7::letterbox_workspace_bytes(new_h, new_w);
+}
+
+int yv7_letterbox(const void* src, int B, int H, int W, int new_h, int new_w, int top, int left, int out_h,
+                  int out_w, int pad_b, int pad_g, int pad_r, int out_kind, void* dst, void* workspace,
+                  size_t ws_bytes, void* stream) {
+  if (!src || !dst || !workspace) return fail(YV7_E_ARG, "yv7_letterbox: null argument");
+  if (out_kind < 0 || out_kind > 2) return fail(YV7_E_ARG, "yv7_letterbox: out_kind must be 0, 1 or 2");
+  if (B <= 0 || H <= 0 || W <= 0 || new_h <= 0 || new_w <= 0 || top < 0 || left < 0 || top + new_h > out_h ||
+      left + new_w > out_w)
+    return fail(YV7_E_SHAPE, "yv7_letterbox: the resized image must lie inside the output canvas");
+  if ((size_t)B * H * W * 3 >= ((size_t)1 << 40)) return fail(YV7_E_SHAPE, "yv7_letterbox: input too large");
+  for (int v : {pad_b, pad_g, pad_r})
+    if (v < 0 || v > 255) return fail(YV7_E_ARG, "yv7_letterbox: pad colour outside 0..255");
+  if (ws_bytes < yv7::letterbox_workspace_bytes(new_h, new_w)) return fail(YV7_E_WORKSPACE, "yv7_letterbox: workspace too small");
+  const uint8_t pad[3] = {(uint8_t)pad_b, (uint8_t)pad_g, (uint8_t)pad_r};
+  hipError_t e = yv7::launch_letterbox(reinterpret_cast<const uint8_t*>(src), B, H, W, new_h, new_w, top, left, out_h,
+                                       out_w, pad, out_kind, dst, workspace, reinterpret_cast<hipStream_t>(stream));
+  if (e != hipSuccess) return hip_fail(e, "yv7_letterbox launch");
   return 0;
 }
 

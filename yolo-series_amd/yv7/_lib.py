@@ -62,6 +62,8 @@ SIGNATURES = {
     'yv7_nms': (_i, [_vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     'yv7_end2end_workspace_bytes': (_sz, [_i, _i, _i, _i]),
     'yv7_end2end': (_i, [_vp, _i, _i, _i, _f, _f, _i, _vp, _vp, _vp, _vp, _vp, _sz, _vp]),
+    'yv7_letterbox_workspace_bytes': (_sz, [_i, _i]),
+    'yv7_letterbox': (_i, [_vp, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _i, _vp, _vp, _sz, _vp]),
 }
 
 _LIB = None
