@@ -53,8 +53,12 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(model_name, img, seconds):
-    """The oracle (reference CPU path restated) on host cores: forward + NMS per frame, batch 1."""
+def cpu_baseline(model_name, img, seconds, plan=None, dev=None, parity_frames=4):
+    """The oracle (reference CPU path restated) on host cores: forward + NMS per frame, batch 1.
+
+    Also the metric's parity half: on `parity_frames` synthetic frames the oracle's fp32 detections
+    (detect.py settings, conf 0.25 / iou 0.45) are the ground truth for the GPU fp16 plan's
+    detections, scored with the product's test.py-style mAP (utils/metrics.py)."""
     from oracle import nms_ref, yolo_ref
     from models.yolo import Model
     from yv7.synthetic import synthetic_frames, synthetic_state_dict
@@ -75,9 +79,26 @@ def cpu_baseline(model_name, img, seconds):
             if time.time() - t0 >= seconds and n >= 2:
                 break
         dt = time.time() - t0
-    return {'value': round(n / dt, 3), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
-            'sample': f'{n} frames of {model_name} {img}x{img}, batch 1, fp32 NCHW, forward + NMS '
-                      f'(conf 0.25, iou 0.45), {dt:.1f} s, torch {torch.__version__} CPU'}
+    out = {'value': round(n / dt, 3), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
+           'sample': f'{n} frames of {model_name} {img}x{img}, batch 1, fp32 NCHW, forward + NMS '
+                     f'(conf 0.25, iou 0.45), {dt:.1f} s, torch {torch.__version__} CPU'}
+    if plan is not None and parity_frames > 0:
+        from utils.general import nms_batched
+        from utils.metrics import dets_as_labels, map_from_lists
+        xs = synthetic_frames(parity_frames, img, img, seed=7)
+        with torch.no_grad():
+            zr = torch.cat([yolo_ref.forward(net, fused, xs[i:i + 1])[0] for i in range(parity_frames)])
+        labels = [dets_as_labels(d) for d in nms_ref.non_max_suppression(zr, 0.25, 0.45)]
+        N = plan.num_rows(img, img)
+        zg = torch.empty((parity_frames, N, plan.no), dtype=torch.float32, device=dev)
+        plan.forward_into(xs.to(dev).to(torch.float16 if plan.dtype == 1 else torch.float32), zg)
+        det, _, cnt = nms_batched(zg, 0.25, 0.45)
+        preds = [det[i, :int(cnt[i])].cpu() for i in range(parity_frames)]
+        m50, m5095 = map_from_lists(preds, labels)
+        out['map_parity'] = {'map50': round(m50, 4), 'map50_95': round(m5095, 4), 'frames': parity_frames,
+                             'truth': 'oracle fp32 CPU detections (conf 0.25, iou 0.45)',
+                             'pred': 'libyv7 plan + GPU NMS, same frames and weights'}
+    return out
 
 
 def main():
@@ -217,7 +238,9 @@ def main():
                        'profiled_forwards': nf, 'hip_graph': graph is not None},
         }
         if not a.no_cpu_baseline and world == 1:
-            res['cpu_baseline'] = cpu_baseline(a.model, a.img, a.cpu_seconds)
+            res['cpu_baseline'] = cpu_baseline(a.model, a.img, a.cpu_seconds, plan=plan, dev=dev)
+            if 'map_parity' in res['cpu_baseline']:
+                res['map50_parity'] = res['cpu_baseline']['map_parity']['map50']
         print(json.dumps(res), flush=True)
     if distributed:
         dist.barrier()
