@@ -48,6 +48,9 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='bounded CPU-baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-live-events', action='store_true', help='diagnostic: time the steps without per-op HIP events')
+    ap.add_argument('--split', type=int, default=1, help='run the batch as this many concurrent sub-batches, '
+                    'each on its own HIP stream and workspace (fills the low-resolution layers\' tails and the '
+                    'kernel-boundary gaps of one stream with the other\'s work)')
     ap.add_argument('--graph', action='store_true', help='replay the step as a HIP graph (measured: same speed '
                     'as eager launches on MI355X, the inter-kernel gaps are dependency drains, not launch cost)')
     return ap.parse_args()
@@ -120,9 +123,11 @@ def main():
 
     torch.manual_seed(0)
     dt = torch.float16 if a.dtype == 'f16' else torch.float32
-    model = Model(a.model)
-    synthetic_state_dict(model, seed=0)
-    model = model.float().fuse().eval()
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):   # Model.fuse() prints like the reference; stdout is the JSON line
+        model = Model(a.model)
+        synthetic_state_dict(model, seed=0)
+        model = model.float().fuse().eval()
     if distributed:
         plan = ydist.broadcast_weights(model, dev, dt)
     else:
@@ -138,8 +143,27 @@ def main():
     cnt = torch.empty((B,), dtype=torch.int32, device=dev)
     rowbest = torch.empty((B, N, 4), dtype=torch.float32, device=dev)   # yv7_row_best records
 
+    nsplit = max(1, a.split)
+    if B % nsplit:
+        raise SystemExit(f'--split {nsplit} must divide the batch {B}')
+    sub = B // nsplit
+    streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nsplit - 1)]
+
+    def forward():
+        if nsplit == 1:
+            plan.forward_into(x, z, rowbest=rowbest)
+            return
+        main = streams[0]
+        for s_ in streams[1:]:
+            s_.wait_stream(main)
+        for i, s_ in enumerate(streams):
+            sl = slice(i * sub, (i + 1) * sub)
+            plan.forward_into(x[sl], z[sl], rowbest=rowbest[sl], stream=s_.cuda_stream, ws_slot=i)
+        for s_ in streams[1:]:
+            main.wait_stream(s_)
+
     def step():
-        plan.forward_into(x, z, rowbest=rowbest)
+        forward()
         nms_batched(z, 0.25, 0.45, out=(det, src, cnt), rowbest=rowbest)
         if distributed:
             ydist.gather_detections(det, src, cnt)
@@ -163,7 +187,9 @@ def main():
             step()
         graph.replay()
         torch.cuda.synchronize()
-    n_live = 0 if a.no_live_events else min(a.steps, 2)
+    # with --split the per-op events would time overlapping kernels of two streams: they are taken on
+    # two whole-batch forwards after the timed steps instead
+    n_live = 0 if (a.no_live_events or nsplit > 1) else min(a.steps, 2)
     plan.profile_enable(n_live)
     if distributed:
         dist.barrier()
@@ -183,6 +209,11 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
+    if nsplit > 1 and not a.no_live_events:
+        plan.profile_enable(2)
+        for _ in range(2):
+            plan.forward_into(x, z, rowbest=rowbest)
+        torch.cuda.synchronize()
     nf, op_ms = plan.profile_read()
     plan.profile_enable(0)
     costs = plan.op_costs(B, H, W, x_bytes=x.element_size(), with_raw=False)
@@ -235,7 +266,7 @@ def main():
                          'mfma_frac': round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4)},
             'detail': {'forward_ms_events': round(fwd_ms, 3), 'conv_ms_events': round(conv_ms, 3),
                        'mean_dets_per_image': round(count_mean, 1), 'rows_per_image': N,
-                       'profiled_forwards': nf, 'hip_graph': graph is not None},
+                       'profiled_forwards': nf, 'hip_graph': graph is not None, 'sub_batches': nsplit},
         }
         if not a.no_cpu_baseline and world == 1:
             res['cpu_baseline'] = cpu_baseline(a.model, a.img, a.cpu_seconds, plan=plan, dev=dev)

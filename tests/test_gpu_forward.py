@@ -96,7 +96,7 @@ def test_forward_fp16_layerwise_scale():
     assert worst < 0.05
 
 
-@pytest.mark.parametrize('name', ['yolov7', 'yolov7-tiny'])
+@pytest.mark.parametrize('name', ['yolov7', 'yolov7-tiny', 'yolov7-w6'])
 def test_forward_fp16_map_parity(name):
     """fp16 plan judged like the reference's half() path (BASELINE metric: mAP@0.5 parity vs ref):
     mAP@0.5 of the GPU fp16 detections against the oracle's fp32 detections taken as ground truth

@@ -67,7 +67,8 @@ __device__ __forceinline__ uint32_t a_origin(const ConvParams& p, int b, int ho,
   return (uint32_t)((pix_index(b, ho * p.s - p.pad, wo * p.s - p.pad, p.H, p.W) * p.xc + p.xoff + chunk * 8) * 2);
 }
 
-// The K-step cursor: tap (rr, ss) and channel ci of a K position, advanced 64 at a time.
+// The K-step cursor: tap (rr, ss) and channel ci of a K position, advanced BK at a time.
+template <int BK = BKE>
 struct KCursor {
   int ci, rr, ss, tap;
   __device__ __forceinline__ void init(const ConvParams& p, int k) {
@@ -75,7 +76,7 @@ struct KCursor {
     while (ci >= p.cin) { ci -= p.cin; ++tap; if (++ss == p.k) { ss = 0; ++rr; } }
   }
   __device__ __forceinline__ void advance(const ConvParams& p) {
-    ci += BKE;
+    ci += BK;
     while (ci >= p.cin) { ci -= p.cin; ++tap; if (++ss == p.k) { ss = 0; ++rr; } }
   }
   // byte offset of (rr, ss, ci) relative to the receptive-field origin
@@ -84,31 +85,31 @@ struct KCursor {
   }
 };
 
-// A-operand source of one K step for RA rows: uniform case (1x1, or cin % 64 == 0) = per-row offset
-// + scalar step offset; otherwise per-lane tap tracking (cin of 8..56: tiny's narrow layers).
-template <bool ONE, int RA>
+// A-operand source of one K step (BK deep) for RA rows: uniform case (1x1, or cin % BK == 0) = per-row
+// offset + scalar step offset; otherwise per-lane tap tracking (cin of 8..56: tiny's narrow layers).
+template <bool ONE, int RA, int BK = BKE>
 struct AWalk {
   uint32_t off[RA];   // row origin + this lane's chunk
-  KCursor su;         // uniform cursor (k = kt*64)
-  KCursor ln;         // per-lane cursor (k = kt*64 + chunk*8), non-uniform case only
+  KCursor<BK> su;     // uniform cursor (k = kt*BK)
+  KCursor<BK> ln;     // per-lane cursor (k = kt*BK + chunk*8), non-uniform case only
   bool uni;
   int c16;
   __device__ __forceinline__ void init(const ConvParams& p, int chunk, int kt0 = 0) {
-    uni = ONE || (p.cin & 63) == 0;
+    uni = ONE || (p.cin % BK) == 0;
     c16 = chunk * 16;
-    su.init(p, kt0 * BKE);
-    if (!uni) ln.init(p, kt0 * BKE + chunk * 8);
+    su.init(p, kt0 * BK);
+    if (!uni) ln.init(p, kt0 * BK + chunk * 8);
   }
   // voffset / soffset of row j for step kt (call step() once per K step, in order)
   template <typename F>
   __device__ __forceinline__ void step(const ConvParams& p, int kt, F&& load) {
     if (ONE) {
-      const uint32_t so = (uint32_t)kt * BKE * 2;
-      if ((kt + 1) * BKE <= p.K) {
+      const uint32_t so = (uint32_t)kt * BK * 2;
+      if ((kt + 1) * BK <= p.K) {
 #pragma unroll
         for (int j = 0; j < RA; ++j) load(j, off[j], so);
-      } else {   // ragged last step (cin % 64 != 0): lanes past K read zeros
-        const bool kin = kt * BKE + c16 / 2 < p.K;
+      } else {   // ragged last step (cin % BK != 0): lanes past K read zeros
+        const bool kin = kt * BK + c16 / 2 < p.K;
 #pragma unroll
         for (int j = 0; j < RA; ++j) load(j, kin ? off[j] : OOB, so);
       }
@@ -118,7 +119,7 @@ struct AWalk {
 #pragma unroll
       for (int j = 0; j < RA; ++j) load(j, off[j], so);
     } else {
-      const bool kin = kt * BKE + c16 / 2 < p.K;
+      const bool kin = kt * BK + c16 / 2 < p.K;
       const uint32_t d = ln.offset(p) - (uint32_t)c16;
       ln.advance(p);
 #pragma unroll
@@ -127,6 +128,16 @@ struct AWalk {
   }
 };
 
+// LDS image of a BK-deep stage: rows of BK*2 bytes in 16-byte chunks, the chunk index XOR-swizzled
+// per row so that the 16-lane groups of every ds_read_b128 (lanes (g, li) read chunk g of rows
+// base + li) hit 16 distinct 4-bank groups.  BK 64: 8 chunks per row, key row & 7.  BK 32: 4 chunks
+// per 64-byte row (4 rows per 256-byte bank sweep), key (-(row >> 2)) & 3 (found by exhaustive
+// check of the four lane groups of ds_read_b128).
+template <int BK>
+__device__ __forceinline__ int swz_bk(int row, int chunk) {
+  if constexpr (BK == 64) return chunk ^ (row & 7);
+  else return chunk ^ ((-(row >> 2)) & 3);
+}
 
 // ---------------------------------------------------------------------------------------------
 // Fused Detect epilogue (models/yolo.py:52-57, IDetect.fuseforward yolo.py:140-176) shared by the
@@ -804,18 +815,22 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
 //    LDS staging;
 //  * counted vmcnt waits: the loads younger than the awaited stage are the next stages and, right
 //    after a tile boundary, the previous tile's stores (their number is known per step).
-template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int ACT>
-__global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 76 * 1024) ? 2 : 1) void conv_f16_pring_kernel(
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int ACT, int BK>
+__global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 1024) ? 2 : 1) void conv_f16_pring_kernel(
     const ConvParams p) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
   constexpr int WTM = BM / WM, WTN = BN / WN;
   constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int RA = BM / 8 / NW, RB = BN / 8 / NW;
-  static_assert(RA * 8 * NW == BM && RB * 8 * NW == BN, "tile rows must split into 8-row groups per wave");
+  constexpr int RB_ = BK * 2;              // LDS bytes per tile row
+  constexpr int CPR = RB_ / 16;            // 16-byte chunks per row
+  constexpr int RPI = 64 / CPR;            // tile rows per DMA wave-instruction (1 KiB)
+  constexpr int RA = BM / RPI / NW, RB = BN / RPI / NW;
+  static_assert(RA * RPI * NW == BM && RB * RPI * NW == BN, "tile rows must split into DMA groups per wave");
   static_assert(TN % 2 == 0, "the epilogue pairs 16-channel groups");
+  static_assert(STAGES >= 2 && STAGES <= 4, "counted waits cover up to two stages in flight");
   constexpr int PER = RA + RB;
   constexpr int NST = TM * TN / 2;   // epilogue stores per lane per tile
-  constexpr int STAGE = (BM + BN) * ROWB;
+  constexpr int STAGE = (BM + BN) * RB_;
   constexpr int BIAS = 4096;         // bias vector (<= 1024 channels) behind the ring
   __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + BIAS];
   float* bias_l = reinterpret_cast<float*>(smem + STAGES * STAGE);
@@ -824,12 +839,13 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 76 * 102
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, li = lane & 15;
-  const int lr = lane >> 3, c = (lane & 7) ^ lr;
+  const int lr = lane / CPR;                          // row within the DMA group
+  const int c = swz_bk<BK>(lr, lane % CPR);           // source chunk this lane fetches (slot = lane % CPR)
 
   const int nN = (p.cout + BN - 1) / BN;
   const int T = ((p.M + BM - 1) / BM) * nN;
   const int G = gridDim.x;
-  const int nk = p.kpad / BKE;
+  const int nk = p.kpad / BK;
   const int ntl = (T - (int)blockIdx.x + G - 1) / G;
   const int nsteps = ntl * nk;
 
@@ -840,7 +856,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 76 * 102
   for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
 
   // ---- issue cursor: global step ig = (local tile it, step ikt)
-  AWalk<ONE, RA> aw;
+  AWalk<ONE, RA, BK> aw;
   uint32_t b_off[RB];
   int ig = 0, it = 0, ikt = 0;
   auto issue_next = [&]() {
@@ -848,21 +864,21 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 76 * 102
       const int t = blockIdx.x + it * G;
       const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
       aw.init(p, c, 0);
-      PixelWalk pw(p, m0 + wave * 8 + lr);
+      PixelWalk pw(p, m0 + wave * RPI + lr);
 #pragma unroll
       for (int j = 0; j < RA; ++j) {
-        if (j) pw.advance(p, NW * 8);
+        if (j) pw.advance(p, NW * RPI);
         aw.off[j] = a_origin(p, pw.b, pw.ho, pw.wo, c);
       }
 #pragma unroll
-      for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)(((n0 + (j * NW + wave) * 8 + lr) * p.kpad + c * 8) * 2);
+      for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)(((n0 + (j * NW + wave) * RPI + lr) * p.kpad + c * 8) * 2);
     }
     const int slot = ig % STAGES;
     unsigned char* As = smem + slot * STAGE;
-    unsigned char* Bs = As + BM * ROWB;
-    aw.step(p, ikt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * 8 * ROWB, vo, so); });
+    unsigned char* Bs = As + BM * RB_;
+    aw.step(p, ikt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * RPI * RB_, vo, so); });
 #pragma unroll
-    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * 8 * ROWB, b_off[j], (uint32_t)ikt * BKE * 2);
+    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * RPI * RB_, b_off[j], (uint32_t)ikt * BK * 2);
     ++ig;
     if (++ikt == nk) { ikt = 0; ++it; }
   };
@@ -937,20 +953,20 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 76 * 102
     __builtin_amdgcn_s_barrier();
     if (ig < nsteps) issue_next();   // refills the slot every wave finished reading at step gs-1
     const unsigned char* As = smem + (gs % STAGES) * STAGE;
-    const unsigned char* Bs = As + BM * ROWB;
+    const unsigned char* Bs = As + BM * RB_;
 #pragma unroll
-    for (int sb = 0; sb < 2; ++sb) {
+    for (int sb = 0; sb < BK / 32; ++sb) {
       const int ch = sb * 4 + g;
       u4 xa[TM], wb[TN];
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) {
         const int row = wm * WTM + ii * 16 + li;
-        xa[ii] = *reinterpret_cast<const u4*>(As + row * ROWB + swz(row, ch) * 16);
+        xa[ii] = *reinterpret_cast<const u4*>(As + row * RB_ + swz_bk<BK>(row, ch) * 16);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WTN + j * 16 + li;
-        wb[j] = *reinterpret_cast<const u4*>(Bs + row * ROWB + swz(row, ch) * 16);
+        wb[j] = *reinterpret_cast<const u4*>(Bs + row * RB_ + swz_bk<BK>(row, ch) * 16);
       }
       __builtin_amdgcn_s_setprio(1);
 #pragma unroll
@@ -970,14 +986,14 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 76 * 102
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES, bool ONE>
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int BK>
 hipError_t launch_pring_act(const ConvParams& p, int grid, hipStream_t st) {
   if (p.act == 1)
-    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 1>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 1, BK>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   else if (p.act == 2)
-    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 2>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 2, BK>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   else
-    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 0>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 0, BK>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
 }
 
@@ -993,13 +1009,13 @@ int device_cus() {
 }
 
 // occ: resident blocks per CU the grid is sized for
-template <int BM, int BN, int WM, int WN, int STAGES>
+template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
 hipError_t launch_pring(const ConvParams& p, bool one, int occ, hipStream_t st) {
   if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8) return hipErrorInvalidValue;
   const long T = (long)((p.M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
   const int grid = (int)(T < (long)device_cus() * occ ? T : (long)device_cus() * occ);
-  return one ? launch_pring_act<BM, BN, WM, WN, STAGES, true>(p, grid, st)
-             : launch_pring_act<BM, BN, WM, WN, STAGES, false>(p, grid, st);
+  return one ? launch_pring_act<BM, BN, WM, WN, STAGES, true, BK>(p, grid, st)
+             : launch_pring_act<BM, BN, WM, WN, STAGES, false, BK>(p, grid, st);
 }
 
 template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, bool DET = false>
@@ -1145,6 +1161,11 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 204) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     if (variant == 205) return launch_pring<256, 128, 4, 2, 2>(p, one, 1, st);
     if (variant == 206) return launch_pring<128, 256, 2, 4, 2>(p, one, 1, st);
+    // BK 32 rings: twice the stages in the same LDS (more K steps in flight)
+    if (variant == 211) return launch_pring<256, 256, 2, 4, 4, 32>(p, one, 1, st);
+    if (variant == 212) return launch_pring<256, 128, 4, 2, 4, 32>(p, one, 1, st);
+    if (variant == 213) return launch_pring<128, 128, 2, 2, 4, 32>(p, one, 2, st);
+    if (variant == 214) return launch_pring<256, 256, 2, 4, 3, 32>(p, one, 1, st);
   }
   if (!det && p.cout > 32) {
     // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/

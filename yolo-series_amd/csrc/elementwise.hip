@@ -120,9 +120,116 @@ __global__ __launch_bounds__(NT) void copy_kernel(const T* __restrict__ x, int B
   }
 }
 
+
+// ---- SPPCSPC pool cascade (common.py:271, 276-280 with k = (5, 9, 13)): the three stride-1 pools
+//      p5 = pool5(x), p9 = pool5(p5), p13 = pool5(p9) (max is associative; -inf padding keeps the
+//      cascade exact) in one launch.  Block = one image x 32 channels: the whole H x W x 32 plane
+//      is staged in LDS once and ping-pongs between two buffers, each pool reads LDS only; every
+//      stage's output also leaves as 16-byte stores into its concat slice.  Needs H*W <= 512 (fp16).
+template <typename T>
+__global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x, int B, int H, int W, int xc,
+                                                         int coff, int C, T* __restrict__ y) {
+  constexpr int V = Vec<T>::N;
+  constexpr int CG = 32;                 // channels per block
+  constexpr int NCH = CG / V;            // 16-byte chunks per pixel
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int groups = C / CG;
+  const int b = blockIdx.x / groups, c0 = (blockIdx.x - b * groups) * CG;
+  const int npx = H * W, items = npx * NCH;
+  u4* buf0 = reinterpret_cast<u4*>(lds);
+  u4* buf1 = buf0 + items;
+  for (int i = threadIdx.x; i < items; i += NT) {
+    const int px = i / NCH, ch = i - px * NCH, h = px / W, w = px - h * W;
+    buf0[i] = *reinterpret_cast<const u4*>(x + pix_index(b, h, w, H, W) * xc + coff + c0 + ch * V);
+  }
+  __syncthreads();
+  u4* src = buf0;
+  u4* dst = buf1;
+  for (int stage = 1; stage <= 3; ++stage) {
+    for (int i = threadIdx.x; i < items; i += NT) {
+      const int px = i / NCH, ch = i - px * NCH, h = px / W, w = px - h * W;
+      // 25 independent LDS reads (taps outside the image re-read the centre: max is idempotent)
+      u4 tv[25];
+#pragma unroll
+      for (int dy = -2; dy <= 2; ++dy)
+#pragma unroll
+        for (int dx = -2; dx <= 2; ++dx) {
+          const int hi = h + dy, wi = w + dx;
+          const bool in = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
+          tv[(dy + 2) * 5 + dx + 2] = src[(in ? hi * W + wi : px) * NCH + ch];
+        }
+      u4 o;
+      if constexpr (sizeof(T) == 2) {   // packed fp16 max (v_pk_max_f16), 8 channels per 4 ops
+        typedef _Float16 hv8 __attribute__((ext_vector_type(8)));
+        hv8 m = __builtin_bit_cast(hv8, tv[0]);
+#pragma unroll
+        for (int k = 1; k < 25; ++k) m = __builtin_elementwise_max(m, __builtin_bit_cast(hv8, tv[k]));
+        o = __builtin_bit_cast(u4, m);
+      } else {
+        T m[V];
+#pragma unroll
+        for (int e = 0; e < V; ++e) m[e] = neg_inf<T>();
+#pragma unroll
+        for (int k = 0; k < 25; ++k) {
+          const T* e = reinterpret_cast<const T*>(&tv[k]);
+#pragma unroll
+          for (int q = 0; q < V; ++q) m[q] = tmax(m[q], e[q]);
+        }
+        o = *reinterpret_cast<const u4*>(m);
+      }
+      dst[i] = o;
+      *reinterpret_cast<u4*>(y + pix_index(b, h, w, H, W) * xc + coff + stage * C + c0 + ch * V) = o;
+    }
+    __syncthreads();
+    u4* t = src;
+    src = dst;
+    dst = t;
+  }
+}
+
+
+// ---- ReOrg input packing, vectorised (fp16 plans, yc == 16): one thread per output pixel reads its
+//      2 x 2 x 3 source values as three 2-value rows pairs (4-byte loads, coalesced along the row)
+//      and writes the 16 channels (12 + 4 zero) as two 16-byte stores.
+template <typename S>
+__global__ __launch_bounds__(NT) void input_reorg16_kernel(const S* __restrict__ x, _Float16* __restrict__ y, int B,
+                                                          int H, int W) {
+  const int Ho = H / 2, Wo = W / 2;
+  const int npix = B * Ho * Wo;
+  const size_t plane = (size_t)H * W;
+  for (int pix = blockIdx.x * NT + threadIdx.x; pix < npix; pix += gridDim.x * NT) {
+    const int t = pix / Wo, wo = pix - t * Wo;
+    const int b = t / Ho, ho = t - b * Ho;
+    const S* xb = x + (size_t)b * 3 * plane + (size_t)(2 * ho) * W + 2 * wo;
+    _Float16 v[16];
+#pragma unroll
+    for (int ch = 0; ch < 3; ++ch) {
+      const S* r0 = xb + ch * plane;
+      const S* r1 = r0 + W;
+      // channel = g*3 + ch, g over (row even,col even),(odd,even),(even,odd),(odd,odd) (common.py:52-53)
+      v[0 * 3 + ch] = (_Float16)(float)r0[0];
+      v[1 * 3 + ch] = (_Float16)(float)r1[0];
+      v[2 * 3 + ch] = (_Float16)(float)r0[1];
+      v[3 * 3 + ch] = (_Float16)(float)r1[1];
+    }
+#pragma unroll
+    for (int c = 12; c < 16; ++c) v[c] = (_Float16)0.0f;
+    u4* out = reinterpret_cast<u4*>(y + pix_index(b, ho, wo, Ho, Wo) * 16);
+    out[0] = *reinterpret_cast<const u4*>(&v[0]);
+    out[1] = *reinterpret_cast<const u4*>(&v[8]);
+  }
+}
+
 template <typename T, typename S>
 hipError_t input_t(const void* x, void* y, int B, int H, int W, int yc, bool reorg, hipStream_t st) {
   const size_t npix = (size_t)B * (reorg ? (H / 2) * (W / 2) : H * W);
+  if constexpr (std::is_same<T, _Float16>::value) {
+    if (reorg && yc == 16) {
+      hipLaunchKernelGGL((input_reorg16_kernel<S>), dim3(grid_for(npix)), dim3(NT), 0, st, (const S*)x, (T*)y, B, H,
+                         W);
+      return hipGetLastError();
+    }
+  }
   if (reorg)
     hipLaunchKernelGGL((input_kernel<T, S, true>), dim3(grid_for(npix)), dim3(NT), 0, st, (const S*)x, (T*)y, B, H,
                        W, yc);
@@ -176,6 +283,26 @@ hipError_t launch_copy(int dtype, const void* x, int B, int H, int W, int xc, in
   else
     hipLaunchKernelGGL(copy_kernel<float>, dim3(grid_for(work)), dim3(NT), 0, st, (const float*)x, B, H, W, xc, xoff,
                        (float*)y, yc, yoff, C);
+  return hipGetLastError();
+}
+
+bool spp_cascade_supported(int dtype, int H, int W, int C) {
+  const int V = dtype == 1 ? 8 : 4;
+  return C % 32 == 0 && (size_t)2 * H * W * (32 / V) * 16 <= 64 * 1024;
+}
+
+// x: the concat tensor (pitch xc) holding the pool input at channel slice [coff, coff + C); the three
+// pools go to [coff + C, coff + 2C), [coff + 2C, coff + 3C), [coff + 3C, coff + 4C) of the same tensor.
+hipError_t launch_spp_cascade(int dtype, void* x, int B, int H, int W, int xc, int coff, int C, hipStream_t st) {
+  const int V = dtype == 1 ? 8 : 4;
+  const size_t lds = (size_t)2 * H * W * (32 / V) * 16;
+  const dim3 grid(B * (C / 32));
+  if (dtype == 1)
+    hipLaunchKernelGGL(spp_cascade_kernel<_Float16>, grid, dim3(NT), lds, st, (const _Float16*)x, B, H, W, xc, coff, C,
+                       (_Float16*)x);
+  else
+    hipLaunchKernelGGL(spp_cascade_kernel<float>, grid, dim3(NT), lds, st, (const float*)x, B, H, W, xc, coff, C,
+                       (float*)x);
   return hipGetLastError();
 }
 

@@ -39,9 +39,9 @@ struct yv7_plan {
   void* weights = nullptr;
   size_t wbytes = 0;
   void* zero = nullptr;  // 4 KiB of zeros
-  // the workspace whose zero frames are known to be intact (see yv7_forward)
-  const void* ws_ready = nullptr;
-  size_t ws_ready_bytes = 0;
+  // the workspaces (pointer, layout size) whose zero frames are known to be intact (see yv7_forward);
+  // several, so that sub-batches can run concurrently on their own streams and workspaces
+  std::vector<std::pair<const void*, size_t>> ws_ready;
   // live profiling: events[f * (n_ops + 1) + i]
   std::vector<hipEvent_t> events;
   int prof_max = 0, prof_used = 0;
@@ -344,10 +344,23 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   hipError_t e = hipSuccess;
   // Kernels write only tensor interiors, so the zero frames survive from one forward to the next:
   // the workspace is cleared when it is first seen (or its layout changes) and never again.
-  if (ws != p->ws_ready || total != p->ws_ready_bytes) {
-    if ((e = hipMemsetAsync(ws, 0, total, st)) != hipSuccess) return hip_fail(e, "hipMemsetAsync(workspace)");
-    p->ws_ready = ws;
-    p->ws_ready_bytes = total;
+  {
+    bool ready = false;
+    for (auto& w : p->ws_ready)
+      if (w.first == ws && w.second == total) ready = true;
+    if (!ready) {
+      if ((e = hipMemsetAsync(ws, 0, total, st)) != hipSuccess) return hip_fail(e, "hipMemsetAsync(workspace)");
+      // a workspace overlapping this one (another layout of the same memory) is no longer intact
+      const char* lo = reinterpret_cast<const char*>(ws);
+      std::vector<std::pair<const void*, size_t>> keep;
+      for (auto& w : p->ws_ready) {
+        const char* wl = reinterpret_cast<const char*>(w.first);
+        if (wl + w.second <= lo || lo + total <= wl) keep.push_back(w);
+      }
+      keep.emplace_back(ws, total);
+      if (keep.size() > 8) keep.erase(keep.begin());
+      p->ws_ready = keep;
+    }
   }
   const int nrows = (int)yv7_num_rows(p, H, W);
   // raw-logit and z row offsets of each level
@@ -378,6 +391,7 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
     p->prof_used++;
     if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
+  size_t fused_until = 0;   // ops [.., fused_until) were launched as part of a fused group
   for (size_t i = 0; i < p->ops.size(); ++i) {
     const auto& o = p->ops[i];
     switch (o.kind) {
@@ -446,6 +460,24 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
       case YV7_OP_MAXPOOL: {
         const auto& ti = p->tensors[o.src];
         const auto& to = p->tensors[o.dst];
+        // SPPCSPC's cascade (graph.py: pool5 three times, each reading the previous slice of one
+        // concat tensor): one fused launch; the two later ops record no time of their own
+        if (i + 2 < p->ops.size() && !(fused_until > i)) {
+          const auto& o1 = p->ops[i + 1];
+          const auto& o2 = p->ops[i + 2];
+          auto pool5 = [](const yv7_op_desc& q) { return q.kind == YV7_OP_MAXPOOL && q.k == 5 && q.s == 1 && q.pad == 2; };
+          const int Hi = H >> ti.shift, Wi = W >> ti.shift;
+          if (pool5(o) && pool5(o1) && pool5(o2) && o.src == o.dst && o1.src == o.dst && o1.dst == o.dst &&
+              o2.src == o.dst && o2.dst == o.dst && o.dst_coff == o.src_coff + o.cout &&
+              o1.src_coff == o.dst_coff && o1.dst_coff == o1.src_coff + o.cout && o2.src_coff == o1.dst_coff &&
+              o2.dst_coff == o2.src_coff + o.cout && o1.cout == o.cout && o2.cout == o.cout &&
+              yv7::spp_cascade_supported(p->dtype, Hi, Wi, o.cout)) {
+            e = yv7::launch_spp_cascade(p->dtype, wsb + off[o.src], B, Hi, Wi, ti.channels, o.src_coff, o.cout, st);
+            fused_until = i + 3;
+            break;
+          }
+        }
+        if (fused_until > i) break;   // a later op of an already-launched cascade
         const int Hi = H >> ti.shift, Wi = W >> ti.shift;
         const int Ho = (Hi + 2 * o.pad - o.k) / o.s + 1, Wo = (Wi + 2 * o.pad - o.k) / o.s + 1;
         if (Ho != (H >> to.shift) || Wo != (W >> to.shift))

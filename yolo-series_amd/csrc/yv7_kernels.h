@@ -107,6 +107,8 @@ hipError_t launch_input(int dtype, const void* x, int x_dtype, void* y, int B, i
                         bool reorg, hipStream_t st);
 hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int Ho,
                           int Wo, int yc, int yoff, int C, int k, int s, int pad, hipStream_t st);
+bool spp_cascade_supported(int dtype, int H, int W, int C);
+hipError_t launch_spp_cascade(int dtype, void* x, int B, int H, int W, int xc, int coff, int C, hipStream_t st);
 hipError_t launch_upsample2x(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int yc,
                              int yoff, int C, hipStream_t st);
 bool stem_supported(int cin, int ca, int cb, int sa);

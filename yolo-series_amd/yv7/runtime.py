@@ -90,14 +90,17 @@ class Plan:
     def num_rows(self, H, W):
         return int(L.lib().yv7_num_rows(self._h, H, W))
 
-    def workspace(self, B, H, W):
-        key = (B, H, W)
+    def workspace(self, B, H, W, slot=0):
+        """The forward workspace for a [B,3,H,W] batch; `slot` > 0 gives further ones, so that
+        sub-batches can run concurrently on their own streams."""
+        key = (B, H, W, slot)
         ws = self._ws.get(key)
         if ws is None:
             nbytes = L.lib().yv7_workspace_bytes(self._h, B, H, W)
             if nbytes == 0:
                 L.check(-2, f'yv7_workspace_bytes(B={B}, H={H}, W={W})')
-            self._ws.clear()  # keep one shape resident
+            for k in [k for k in self._ws if k[:3] != (B, H, W)]:   # keep one shape resident
+                del self._ws[k]
             ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
         return ws
@@ -175,7 +178,7 @@ class Plan:
                 out.append((kind, 0.0, 2 * B * Hi * Wi * c * es))
         return out
 
-    def forward_into(self, x, z, raw=None, stream=None, rowbest=None):
+    def forward_into(self, x, z, raw=None, stream=None, rowbest=None, ws_slot=0):
         """Forward into caller buffers; rowbest (optional): [B, N, 4] 32-bit yv7_row_best records."""
         B, C, H, W = x.shape
         if C != 3:
@@ -183,7 +186,7 @@ class Plan:
         if x.dtype not in (torch.float32, torch.float16):
             x = x.float()
         x = x.contiguous()
-        ws = self.workspace(B, H, W)
+        ws = self.workspace(B, H, W, ws_slot)
         xdt = L.DT_F16 if x.dtype == torch.float16 else L.DT_F32
         if stream is None:
             stream = torch.cuda.current_stream(self.device).cuda_stream
