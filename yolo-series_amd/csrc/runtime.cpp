@@ -189,7 +189,7 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
         return fail(YV7_E_ARG, "yv7_plan_create: bad detect op");
     }
     if (o.kind == YV7_OP_STEM) {
-      if (d->dtype != YV7_DT_F16 || !yv7::stem_supported(o.cin, o.cout, o.cout2, o.s) || o.k != 3 ||
+      if (d->dtype != YV7_DT_F16 || !yv7::stem_supported(o.cin, o.cout, o.cout2, o.s) || o.k != 3 || o.act != o.act2 ||
           o.dst_coff % vec || o.dst_coff + o.cout2 > d->tensors[o.dst].channels)
         return fail(YV7_E_ARG, "yv7_plan_create: unsupported stem op");
       const size_t wa = (size_t)o.cout * ((27 + 63) / 64 * 64) * 2, wb = (size_t)o.cout2 * ((9 * o.cout + 63) / 64 * 64) * 2;

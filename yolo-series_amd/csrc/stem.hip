@@ -24,7 +24,7 @@ namespace {
 
 constexpr int NT = 256;
 
-template <typename S, int CA, int CB, int SA, int TBY, int TBX>
+template <typename S, int CA, int CB, int SA, int TBY, int TBX, int ACT_A, int ACT_B>
 __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   constexpr int TAY = 2 * TBY + 1, TAX = 2 * TBX + 1;      // conv-A pixels feeding the tile
   constexpr int PY = SA * (TAY - 1) + 3, PX = SA * (TAX - 1) + 3;
@@ -77,53 +77,93 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
     }
     *reinterpret_cast<h4*>(patch + i * 4) = v;
   }
-  // conv-A weights: two 16-row tiles per n-tile pair, K = 32 (k = tap*3 + ci, 27..31 zero)
+  // conv A's K layout on the MFMA: 4 halves per tap (3 channels + the patch's zero 4th channel),
+  // two taps per 8-half lane group, so a lane's A fragment is two 8-byte patch pixels — for the
+  // horizontally adjacent pairs one contiguous 16 bytes — instead of eight scattered halves.
+  //   K step 0: g0 taps (0,0)(0,1), g1 (1,0)(1,1), g2 (2,0)(2,1), g3 (0,2)(1,2);  K step 1: g0 (2,2).
+  // SiLU is folded (ACT_A == 1): conv A's weights and bias are scaled by -log2(e) at load, so the
+  // MFMA yields z = -log2(e) x, the epilogue stores z * rcp(1 + 2^z) = -log2(e) * silu(x), and conv B
+  // compensates with its bias scaled by -log2(e) (then it too yields -log2(e) x_B).
+  constexpr float NLOG2E = -1.4426950408889634f;
+  const float sa_scale = ACT_A == 1 ? NLOG2E : 1.0f;
+  const float sb_scale = ACT_A == 1 ? NLOG2E : 1.0f;   // conv B's pre-activation scale
+  auto tap_of = [](int ks, int gg, int half) -> int {   // (r*3 + s) of lane group gg, half 0/1; -1 = none
+    if (ks == 0) {
+      if (gg < 3) return gg * 3 + half;                 // (gg, 0), (gg, 1)
+      return half == 0 ? 2 : 5;                         // (0, 2), (1, 2)
+    }
+    return (gg == 0 && half == 0) ? 8 : -1;             // (2, 2)
+  };
   constexpr int NAT = CA / 16;
-  u4 wa[NAT];
+  u4 wa[2][NAT];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < NAT; ++nt) {
+      typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+      h8v w8;
+      const _Float16* wrow = reinterpret_cast<const _Float16*>(p.wa) + (size_t)(nt * 16 + li) * p.kpad_a;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int tap = tap_of(ks, g, h2);
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci)
+          w8[h2 * 4 + ci] = (tap >= 0 && ci < 3) ? (_Float16)((float)wrow[tap * 3 + ci] * sa_scale) : (_Float16)0.f;
+      }
+      wa[ks][nt] = __builtin_bit_cast(u4, w8);
+    }
+  // patch byte offsets (relative to the A-pixel's patch origin) of this lane's two taps per K step
+  int toff[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int tap = tap_of(ks, g, h2);
+      toff[ks][h2] = tap >= 0 ? ((tap / 3) * PX + tap % 3) * 8 : -1;
+    }
+  float ba_l[NAT][4];
 #pragma unroll
   for (int nt = 0; nt < NAT; ++nt)
-    wa[nt] = *reinterpret_cast<const u4*>(reinterpret_cast<const _Float16*>(p.wa) + (size_t)(nt * 16 + li) * p.kpad_a + g * 8);
-  // per-lane gather offsets of its 8 k values (in halves, relative to the A-pixel's patch origin)
-  int koff[8];
 #pragma unroll
-  for (int kk = 0; kk < 8; ++kk) {
-    const int k = g * 8 + kk;
-    const int tap = k / 3, ci = k - tap * 3, r = tap / 3, s = tap - r * 3;
-    koff[kk] = k < 27 ? ((r * PX + s) * 4 + ci) : -1;
-  }
+    for (int e = 0; e < 4; ++e) ba_l[nt][e] = p.ba[nt * 16 + g * 4 + e] * sa_scale;
   __syncthreads();
 
   // 2. conv A on MFMA -> abuf
+  const unsigned char* pbytes = reinterpret_cast<const unsigned char*>(patch);
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
   for (int mt = wave; mt < MA; mt += 4) {
     const int m = mt * 16 + li;
     const int mc = m < NA ? m : NA - 1;
     const int yl = mc / TAX, xl = mc - yl * TAX;
-    const int base = (SA * yl * PX + SA * xl) * 4;
-    typedef _Float16 h8v __attribute__((ext_vector_type(8)));
-    h8v xv;
+    const int base = (SA * yl * PX + SA * xl) * 8;
+    u4 xv[2];
 #pragma unroll
-    for (int kk = 0; kk < 8; ++kk) xv[kk] = koff[kk] >= 0 ? patch[base + koff[kk]] : (_Float16)0.f;
+    for (int ks = 0; ks < 2; ++ks) {
+      u2 lo = {0u, 0u}, hi = {0u, 0u};
+      if (toff[ks][0] >= 0) lo = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][0]);
+      if (toff[ks][1] >= 0) hi = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][1]);
+      xv[ks] = u4{lo[0], lo[1], hi[0], hi[1]};
+    }
     const int ay = ay0 + yl, ax = ax0 + xl;
     const bool inside = m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA;
-    f4 acc[NAT];
 #pragma unroll
     for (int nt = 0; nt < NAT; ++nt) {
-      f4 bv;
+      f4 acc = {ba_l[nt][0], ba_l[nt][1], ba_l[nt][2], ba_l[nt][3]};
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[0][nt]), __builtin_bit_cast(h8, xv[0]),
+                                                   acc, 0, 0, 0);
+      acc = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[1][nt]), __builtin_bit_cast(h8, xv[1]),
+                                                   acc, 0, 0, 0);
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      h4 o;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = p.ba[nt * 16 + g * 4 + e];
-      acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[nt]), xv, bv, 0, 0, 0);
-    }
-    with_act(p.act_a, [&](auto actc) {
-      constexpr int ACT = decltype(actc)::value;
-#pragma unroll
-      for (int nt = 0; nt < NAT; ++nt) {
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        h4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = inside ? (_Float16)act_t<ACT>(acc[nt][e]) : (_Float16)0.f;
-        if (m < NA) *reinterpret_cast<h4*>(abuf + m * APITCH + (nt * 16 + g * 4) * 2) = o;
+      for (int e = 0; e < 4; ++e) {
+        float v;
+        if constexpr (ACT_A == 1) v = acc[e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[e]));
+        else v = act_t<ACT_A>(acc[e]);
+        o[e] = inside ? (_Float16)v : (_Float16)0.f;
       }
-    });
+      if (m < NA) *reinterpret_cast<h4*>(abuf + m * APITCH + (nt * 16 + g * 4) * 2) = o;
+    }
   }
   __syncthreads();
 
@@ -133,7 +173,7 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   {
     f4 bv;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) bv[e] = p.bb[wave * 16 + g * 4 + e];
+    for (int e = 0; e < 4; ++e) bv[e] = p.bb[wave * 16 + g * 4 + e] * sb_scale;
 #pragma unroll
     for (int i = 0; i < MB; ++i) acc[i] = bv;
   }
@@ -155,18 +195,23 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   // 4. epilogue via LDS: lane holds 4 consecutive channels of one conv-B pixel
   {
     const int col = wave * 16 + g * 4;
-    with_act(p.act_b, [&](auto actc) {
-      constexpr int ACT = decltype(actc)::value;
+    // acc = sb_scale * x_B: undo the scale (SiLU: x = -ln2 * z, silu = x * rcp(1 + 2^z))
 #pragma unroll
-      for (int i = 0; i < MB; ++i) {
-        const int mb = i * 16 + li;
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        h4 o;
+    for (int i = 0; i < MB; ++i) {
+      const int mb = i * 16 + li;
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      h4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) o[e] = (_Float16)act_t<ACT>(acc[i][e]);
-        *reinterpret_cast<h4*>(smem + mb * CPITCH + col * 2) = o;
+      for (int e = 0; e < 4; ++e) {
+        float v;
+        if constexpr (ACT_A == 1 && ACT_B == 1)
+          v = (acc[i][e] * -0.6931471805599453f) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[i][e]));
+        else
+          v = act_t<ACT_B>(acc[i][e] / sb_scale);
+        o[e] = (_Float16)v;
       }
-    });
+      *reinterpret_cast<h4*>(smem + mb * CPITCH + col * 2) = o;
+    }
   }
   __syncthreads();
   constexpr int CPR = CB * 2 / 16;
@@ -181,13 +226,21 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   }
 }
 
-template <typename S, int CA, int CB, int SA>
+template <typename S, int CA, int CB, int SA, int ACT_A, int ACT_B>
 hipError_t stem_t(const StemParams& p, hipStream_t st) {
   constexpr int TBY = 8, TBX = 16;
   const int HB = p.H / SA / 2, WB = p.W / SA / 2;
   const int nblk = p.B * ((HB + TBY - 1) / TBY) * ((WB + TBX - 1) / TBX);
-  hipLaunchKernelGGL((stem_kernel<S, CA, CB, SA, TBY, TBX>), dim3(nblk), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((stem_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B>), dim3(nblk), dim3(NT), 0, st, p);
   return hipGetLastError();
+}
+
+template <typename S, int CA, int CB, int SA>
+hipError_t stem_acts(const StemParams& p, hipStream_t st) {
+  if (p.act_a == 1 && p.act_b == 1) return stem_t<S, CA, CB, SA, 1, 1>(p, st);
+  if (p.act_a == 2 && p.act_b == 2) return stem_t<S, CA, CB, SA, 2, 2>(p, st);
+  if (p.act_a == 0 && p.act_b == 0) return stem_t<S, CA, CB, SA, 0, 0>(p, st);
+  return hipErrorInvalidValue;   // mixed activations: not a stem the graph compiler emits
 }
 
 }  // namespace
@@ -198,8 +251,8 @@ bool stem_supported(int cin, int ca, int cb, int sa) {
 
 hipError_t launch_stem(const StemParams& p, int x_dtype, hipStream_t st) {
   if (p.sa == 1)
-    return x_dtype == 1 ? stem_t<_Float16, 32, 64, 1>(p, st) : stem_t<float, 32, 64, 1>(p, st);
-  return x_dtype == 1 ? stem_t<_Float16, 32, 64, 2>(p, st) : stem_t<float, 32, 64, 2>(p, st);
+    return x_dtype == 1 ? stem_acts<_Float16, 32, 64, 1>(p, st) : stem_acts<float, 32, 64, 1>(p, st);
+  return x_dtype == 1 ? stem_acts<_Float16, 32, 64, 2>(p, st) : stem_acts<float, 32, 64, 2>(p, st);
 }
 
 }  // namespace yv7

@@ -132,7 +132,7 @@ def _stem_candidate(layers, dtype):
     c0, c1 = l0.conv, l1.conv
     if not (c0.in_channels == 3 and c0.out_channels == 32 and c0.kernel_size[0] == 3 and c0.stride[0] in (1, 2)
             and c0.padding[0] == 1 and c1.out_channels == 64 and c1.kernel_size[0] == 3 and c1.stride[0] == 2
-            and c1.padding[0] == 1 and c0.groups == 1 and c1.groups == 1):
+            and c1.padding[0] == 1 and c0.groups == 1 and c1.groups == 1 and _act_code(l0.act) == _act_code(l1.act)):
         return None
     for m in layers[2:]:
         srcs = [m.f] if isinstance(m.f, int) else list(m.f)
