@@ -876,9 +876,11 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
     const int slot = ig % STAGES;
     unsigned char* As = smem + slot * STAGE;
     unsigned char* Bs = As + BM * RB_;
-    aw.step(p, ikt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * RPI * RB_, vo, so); });
+    if (p.variant != 298) {   // 298: microbenchmark hook, no operand traffic (times the rest)
+      aw.step(p, ikt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * RPI * RB_, vo, so); });
 #pragma unroll
-    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * RPI * RB_, b_off[j], (uint32_t)ikt * BK * 2);
+      for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * RPI * RB_, b_off[j], (uint32_t)ikt * BK * 2);
+    }
     ++ig;
     if (++ikt == nk) { ikt = 0; ++it; }
   };
@@ -954,29 +956,34 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
     if (ig < nsteps) issue_next();   // refills the slot every wave finished reading at step gs-1
     const unsigned char* As = smem + (gs % STAGES) * STAGE;
     const unsigned char* Bs = As + BM * RB_;
+    // every fragment of the step is read up front: the second sub-step's reads are in flight under
+    // the first sub-step's MFMAs
+    constexpr int NSB = BK / 32;
+    u4 xa[NSB][TM], wb[NSB][TN];
 #pragma unroll
-    for (int sb = 0; sb < BK / 32; ++sb) {
+    for (int sb = 0; sb < NSB; ++sb) {
       const int ch = sb * 4 + g;
-      u4 xa[TM], wb[TN];
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) {
         const int row = wm * WTM + ii * 16 + li;
-        xa[ii] = *reinterpret_cast<const u4*>(As + row * RB_ + swz_bk<BK>(row, ch) * 16);
+        xa[sb][ii] = *reinterpret_cast<const u4*>(As + row * RB_ + swz_bk<BK>(row, ch) * 16);
       }
 #pragma unroll
       for (int j = 0; j < TN; ++j) {
         const int row = wn * WTN + j * 16 + li;
-        wb[j] = *reinterpret_cast<const u4*>(Bs + row * RB_ + swz_bk<BK>(row, ch) * 16);
+        wb[sb][j] = *reinterpret_cast<const u4*>(Bs + row * RB_ + swz_bk<BK>(row, ch) * 16);
       }
-      __builtin_amdgcn_s_setprio(1);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int sb = 0; sb < NSB; ++sb)
 #pragma unroll
       for (int j = 0; j < TN; ++j)
 #pragma unroll
         for (int ii = 0; ii < TM; ++ii)
-          acc[j][ii] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]),
-                                                              __builtin_bit_cast(h8, xa[ii]), acc[j][ii], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-    }
+          acc[j][ii] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[sb][j]),
+                                                              __builtin_bit_cast(h8, xa[sb][ii]), acc[j][ii], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
     if (++ckt == nk) {
       epilogue();
       ckt = 0;
@@ -1145,7 +1152,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // 128->128 @80 86 -> 81, s2 128->128 @160 96 -> 90, 512->512 @20 80 -> 76).
     const long t256 = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
     if (one) {
-      if (p.K >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
+      if (p.K >= 256 && p.cout >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
       if (p.K <= 512 && p.M >= 51200) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     } else if (p.k == 3 && (p.cout == 128 || (p.cout == 512 && p.Ho <= 20))) {
       return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
@@ -1155,7 +1162,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   if (ch.cfg >= 0) return launch_choice(p, ch, one, st);
   if (!det && p.cout > 32) {
     // persistent ring configurations (microbenchmarks: 201..206)
-    if (variant == 201) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
+    if (variant == 201 || variant == 298) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
     if (variant == 202) return launch_pring<256, 128, 4, 2, 3>(p, one, 1, st);
     if (variant == 203) return launch_pring<128, 128, 2, 2, 3>(p, one, 1, st);
     if (variant == 204) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
@@ -1166,6 +1173,10 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 212) return launch_pring<256, 128, 4, 2, 4, 32>(p, one, 1, st);
     if (variant == 213) return launch_pring<128, 128, 2, 2, 4, 32>(p, one, 2, st);
     if (variant == 214) return launch_pring<256, 256, 2, 4, 3, 32>(p, one, 1, st);
+    // 4-wave blocks, two per CU (blocks drift out of phase: one block's epilogue beside the other's MFMAs)
+    if (variant == 215) return launch_pring<256, 128, 2, 2, 3, 32>(p, one, 2, st);
+    if (variant == 216) return launch_pring<128, 256, 2, 2, 3, 32>(p, one, 2, st);
+    if (variant == 217) return launch_pring<128, 128, 2, 2, 2, 64>(p, one, 2, st);
   }
   if (!det && p.cout > 32) {
     // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/
