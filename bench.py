@@ -259,7 +259,8 @@ def main():
             'roofline': {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved_gbs / HBM_PEAK_GBS, 4), 'traffic': traffic,
                          'traffic_unit': 'bytes per launch (PMC, profiles/r1_pmc_traffic.json)',
-                         'kernel': 'conv_kernel (implicit-GEMM MFMA conv, all CONV/DETECT launches)',
+                         'kernel': 'conv kernels (MFMA implicit-GEMM ring / persistent ring / weight-stationary '
+                                   '3x3 / halo; all CONV and DETECT launches of the forward)',
                          'launches_per_forward': nconv, 'mean_launch_us': round(mean_launch_s * 1e6, 2),
                          'algorithmic_bytes_per_launch': round(conv_bytes / nconv),
                          'mfma_tflops': round(achieved_tf, 1),

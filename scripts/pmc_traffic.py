@@ -25,8 +25,9 @@ def load(d, counter):
 
 
 def family(name):
-    for k in ('conv3x3_halo_kernel', 'conv_f16_ring_kernel', 'conv_f16_kernel', 'conv_kernel', 'stem_kernel',
-              'maxpool_kernel', 'upsample_kernel', 'copy_kernel', 'input_kernel', 'nms_'):
+    for k in ('conv3x3_halo_kernel', 'conv3x3_ws64_kernel', 'conv_f16_pring_kernel', 'conv_f16_ring_kernel',
+              'conv_f16_kernel', 'conv_kernel', 'stem_kernel', 'spp_cascade_kernel', 'maxpool_kernel',
+              'upsample_kernel', 'copy_kernel', 'input_reorg16_kernel', 'input_kernel', 'letterbox_kernel', 'nms_'):
         if k in name:
             return k.rstrip('_')
     return re.sub(r'\(.*', '', name)[:40]
@@ -45,7 +46,8 @@ def main(src, dst):
     for f, (n, rb, wb) in sorted(fam.items(), key=lambda kv: -kv[1][1]):
         res['families'][f] = {'launches': n, 'read_bytes_per_launch': rb / n, 'write_bytes_per_launch': wb / n,
                               'hbm_bytes_per_launch': (rb + wb) / n}
-        if f in ('conv3x3_halo_kernel', 'conv_f16_ring_kernel', 'conv_f16_kernel', 'conv_kernel'):
+        if f in ('conv3x3_halo_kernel', 'conv3x3_ws64_kernel', 'conv_f16_pring_kernel', 'conv_f16_ring_kernel',
+                 'conv_f16_kernel', 'conv_kernel'):
             conv_n += n
             conv_b += rb + wb
     res['conv_family'] = {'launches': conv_n, 'hbm_bytes_per_launch': conv_b / max(conv_n, 1)}
