@@ -138,3 +138,19 @@ def non_max_suppression(prediction, conf_thres=0.25, iou_thres=0.45, classes=Non
         output[xi] = x[i]
         rows_out[xi] = rows[i]
     return (output, rows_out) if return_rows else output
+
+
+def scale_coords(img1_shape, coords, img0_shape):
+    """utils/general.py:340-361 (ratio_pad=None): letterboxed xyxy -> original-image pixels, clipped.
+    detect.py:183 then applies .round()."""
+    gain = min(img1_shape[0] / img0_shape[0], img1_shape[1] / img0_shape[1])
+    padw, padh = (img1_shape[1] - img0_shape[1] * gain) / 2, (img1_shape[0] - img0_shape[0] * gain) / 2
+    c = coords.clone()
+    c[:, [0, 2]] -= padw
+    c[:, [1, 3]] -= padh
+    c[:, :4] /= gain
+    c[:, 0].clamp_(0, img0_shape[1])
+    c[:, 1].clamp_(0, img0_shape[0])
+    c[:, 2].clamp_(0, img0_shape[1])
+    c[:, 3].clamp_(0, img0_shape[0])
+    return c

@@ -92,3 +92,57 @@ def letterbox_batch(frames, img_size=640, half=True, color=(114, 114, 114), auto
     geom = letterbox_geometry(tuple(frames.shape[1:3]), img_size, auto, scaleFill, scaleup, stride)
     x = _run(frames, geom, color, OUT_F16_CHW if half else OUT_F32_CHW)
     return x, geom[1], geom[2]
+
+
+# ------------------------------------------------------------------------------------------ images
+IMG_FORMATS = ('bmp', 'jpg', 'jpeg', 'png', 'tif', 'tiff', 'webp', 'mpo')
+
+
+def imread(path):
+    """cv2.imread(path) (BGR uint8 HWC) substitute: cv2 is absent from this image, frames are decoded by
+    PIL.  JPEG decoders may differ from cv2's libjpeg by +-1 per channel (decode parity unpinned);
+    everything after the decode (letterbox, model, NMS) is the path under test."""
+    from PIL import Image
+    with Image.open(path) as im:
+        rgb = np.asarray(im.convert('RGB'))
+    return np.ascontiguousarray(rgb[:, :, ::-1])
+
+
+class LoadImages:
+    """utils/datasets.py:133-202 for image files (a file, a directory or a glob): yields
+    (path, img CHW RGB uint8 letterboxed, img0 HWC BGR, None, ratio, (dw, dh)) like the reference, with
+    the letterbox done on the current HIP device (auto=False, as datasets.py:196)."""
+
+    def __init__(self, path, img_size=640, stride=32):
+        import glob
+        import os
+        p = str(os.path.abspath(path))
+        if '*' in p:
+            files = sorted(glob.glob(p, recursive=True))
+        elif os.path.isdir(p):
+            files = sorted(glob.glob(os.path.join(p, '*.*')))
+        elif os.path.isfile(p):
+            files = [p]
+        else:
+            raise Exception(f'ERROR: {p} does not exist')
+        self.files = [x for x in files if x.split('.')[-1].lower() in IMG_FORMATS]
+        self.img_size, self.stride, self.mode, self.cap = img_size, stride, 'image', None
+        self.nf = len(self.files)
+        assert self.nf > 0, f'No images found in {p}. Supported formats are: {IMG_FORMATS}'
+
+    def __iter__(self):
+        self.count = 0
+        return self
+
+    def __next__(self):
+        if self.count == self.nf:
+            raise StopIteration
+        path = self.files[self.count]
+        self.count += 1
+        img0 = imread(path)
+        img, ratio, dwdh = letterbox(img0, new_shape=(self.img_size, self.img_size), auto=False)
+        img = np.ascontiguousarray(img[:, :, ::-1].transpose(2, 0, 1))   # BGR to RGB, 3 x S x S
+        return path, img, img0, self.cap, ratio, dwdh
+
+    def __len__(self):
+        return self.nf
