@@ -44,7 +44,8 @@ def parse():
     ap.add_argument('--batch', type=int, default=32, help='images per GPU')
     ap.add_argument('--img', type=int, default=640)
     ap.add_argument('--model', default='yolov7')
-    ap.add_argument('--dtype', default='f16', choices=['f16', 'f32'])
+    ap.add_argument('--dtype', default='f16', choices=['f16', 'f32', 'fp8'],
+                    help='fp8: BASELINE configs[4] (1x1 convs on e4m3 weights/activations, fp16 elsewhere)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='bounded CPU-baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-live-events', action='store_true', help='diagnostic: time the steps without per-op HIP events')
@@ -122,13 +123,15 @@ def main():
     from yv7.synthetic import synthetic_state_dict
 
     torch.manual_seed(0)
-    dt = torch.float16 if a.dtype == 'f16' else torch.float32
+    dt = torch.float32 if a.dtype == 'f32' else torch.float16
     import contextlib
     with contextlib.redirect_stdout(sys.stderr):   # Model.fuse() prints like the reference; stdout is the JSON line
         model = Model(a.model)
         synthetic_state_dict(model, seed=0)
         model = model.float().fuse().eval()
-    if distributed:
+    if a.dtype == 'fp8':   # every rank calibrates its own fp8 plan (deterministic: same frames, same scales)
+        plan = Plan.from_model(model, dev, 'fp8')
+    elif distributed:
         plan = ydist.broadcast_weights(model, dev, dt)
     else:
         plan = Plan.from_model(model, dev, dt)

@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define YV7_ABI_VERSION 2
+#define YV7_ABI_VERSION 3
 
 /* Activation tensors in the forward workspace are NHWC with a YV7_BORDER-pixel zero frame around
  * every image: [B][h + 2*YV7_BORDER][w + 2*YV7_BORDER][C].  Kernels write only interiors; the frame
@@ -50,6 +50,11 @@ typedef enum {
 
 typedef enum { YV7_DT_F32 = 0, YV7_DT_F16 = 1 } yv7_dtype;
 typedef enum { YV7_ACT_NONE = 0, YV7_ACT_SILU = 1, YV7_ACT_LEAKY = 2 } yv7_act;
+/* Weight / arithmetic format of one CONV op.  FP8 (fp16 plans, 1x1 stride-1 convs only; BASELINE
+ * configs[4]): weights OCP e4m3 [cout_pad32][cin padded to 128] at w_off with fp32 per-output-channel
+ * scales [cout] at s_off; the fp16 input is quantized per tensor, x8 = e4m3(clamp(x / xscale, +-448)),
+ * and the GEMM runs on the block-scaled fp8 MFMA; y = act(acc * xscale * wscale[c] + bias[c]). */
+typedef enum { YV7_WFMT_PLAN = 0, YV7_WFMT_FP8 = 1 } yv7_wfmt;
 
 typedef enum {
   YV7_OP_INPUT = 0,    /* NCHW image batch -> NHWC tensor; k=2 means fused ReOrg space-to-depth */
@@ -78,6 +83,9 @@ typedef struct {
   int64_t b_off;               /* CONV/DETECT: byte offset of fp32 bias [cout_pad] */
   int32_t cout2, act2;         /* STEM: second conv's output channels / activation */
   int64_t w2_off, b2_off;      /* STEM: second conv's weights / bias */
+  int32_t wfmt;                /* CONV: yv7_wfmt */
+  float xscale;                /* CONV, wfmt FP8: per-tensor input scale (a power of two) */
+  int64_t s_off;               /* CONV, wfmt FP8: byte offset of fp32 weight scales [cout] */
 } yv7_op_desc;
 
 typedef struct {
@@ -138,6 +146,11 @@ int yv7_profile_read(yv7_plan* plan, int* n_forwards, float* op_ms);
  * Lets a caller read any intermediate layer for per-layer parity checks. */
 int yv7_tensor_info(const yv7_plan* plan, int tensor_id, int B, int H, int W, int64_t* offset,
                     int64_t* dims4);
+
+/* Byte range of the fp8 staging buffer inside the forward workspace (the dense e4m3 copy of an FP8
+ * op's input; after a forward it holds the last FP8 op's quantized input).  bytes = 0 when the plan
+ * has no FP8 op.  For parity tests of the quantization. */
+int yv7_f8_scratch_info(const yv7_plan* plan, int B, int H, int W, int64_t* offset, int64_t* bytes);
 
 /* Batched NMS over z [B,N,no] fp32, the semantics of utils/general.py:628-720.
  * det: [B,max_det,6] (x1,y1,x2,y2,conf,cls), src_row: [B,max_det] int64 anchor row of each kept

@@ -261,7 +261,44 @@ def _act(x, act):
     return x
 
 
+def fp8_e4m3(t):
+    """Round to OCP e4m3 (float8_e4m3fn: round to nearest even) with saturation at +-448, back to float."""
+    return t.clamp(-448.0, 448.0).to(torch.float8_e4m3fn).to(t.dtype)
+
+
+def fp8_fused(fused: dict, entries) -> dict:
+    """The fp8 plan's arithmetic (BASELINE configs[4]) as an emulation of the fused network: for every
+    ((layer, SPPCSPC cv index or None), xscale) in `entries`, that 1x1 conv gets per-output-channel e4m3
+    weights (wscale = amax / 448, W ~ e4m3(W / wscale) * wscale) and its input is rounded to e4m3 on the
+    per-tensor scale xscale (x ~ e4m3(x / xscale) * xscale) — see _conv.  Test infrastructure only."""
+    out = {k: (dict(v) if isinstance(v, dict) else v) for k, v in fused.items()}
+    for (layer, sub), xs in entries:
+        w, b = (out[layer] if sub is None else out[layer][sub])[:2]
+        wk = w.reshape(w.shape[0], -1)
+        amax = wk.abs().amax(1)
+        ws = torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+        wq = (fp8_e4m3(wk / ws[:, None]) * ws[:, None]).reshape(w.shape)
+        if sub is None:
+            out[layer] = (wq, b, float(xs))
+        else:
+            out[layer][sub] = (wq, b, float(xs))
+    return out
+
+
+def half_weights(fused: dict) -> dict:
+    """The libyv7 fp16 plan's parameter storage: fp16 weights, fp32 biases; fp8 entries unchanged."""
+    def r(v):
+        if isinstance(v, tuple):
+            return v if len(v) == 3 else (v[0].half().float(), v[1])
+        if isinstance(v, dict):
+            return {j: r(t) for j, t in v.items()}
+        return [r(t) for t in v]
+    return {k: r(v) for k, v in fused.items()}
+
+
 def _conv(x, wb, k, s, pad, act):
+    if len(wb) == 3:   # fp8 emulation entry (fp8_fused): e4m3 input on the per-tensor scale
+        x = fp8_e4m3(x / wb[2]) * wb[2]
     return _act(F.conv2d(x, wb[0], wb[1], s, pad), act)
 
 
@@ -287,6 +324,8 @@ def detect_decode(net: Net, raw: list):
 
 
 def _half_round(v):
+    if isinstance(v, tuple) and len(v) == 3:   # fp8 entry: e4m3 weights with fp32 scales, fp32 bias
+        return v
     if isinstance(v, tuple):
         return (v[0].half().float(), v[1].half().float())
     if isinstance(v, dict):
@@ -348,7 +387,7 @@ def forward64(net: Net, fused: dict, x: torch.Tensor):
     reference's own fp32 z by about |z32 - z64|."""
     def d(v):
         if isinstance(v, tuple):
-            return (v[0].double(), v[1].double())
+            return (v[0].double(), v[1].double()) + tuple(v[2:])
         if isinstance(v, dict):
             return {j: d(t) for j, t in v.items()}
         return [d(t) for t in v]

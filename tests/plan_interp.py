@@ -31,12 +31,21 @@ def _weights(blob, dtype, off, cout, k, cin):
     return raw[:cout, :k * k * cin].reshape(cout, k, k, cin).permute(0, 3, 1, 2).contiguous()
 
 
+def _weights_f8(blob, off, cout, cin, s_off):
+    """FP8 op: e4m3 [cout_pad32][cin padded to 128] times the fp32 per-channel scales -> [cout, cin, 1, 1]."""
+    kp = _rup(cin, 128)
+    raw = blob[off:off + _rup(cout, 32) * kp].view(torch.float8_e4m3fn).float().view(-1, kp)
+    ws = blob[s_off:s_off + 4 * cout].view(torch.float32)
+    return (raw[:cout, :cin] * ws[:, None]).reshape(cout, cin, 1, 1)
+
+
 def _bias(blob, off, cout):
     return blob[off:off + 4 * cout].view(torch.float32).clone()
 
 
-def run(g, x: torch.Tensor):
-    """x: [B, 3, H, W] float -> z [B, N, no] (fp32 math throughout)."""
+def run(g, x: torch.Tensor, return_tensors=False):
+    """x: [B, 3, H, W] float -> z [B, N, no] (fp32 math throughout); with return_tensors also the
+    plan's NCHW tensors (per-op input statistics, e.g. fp8 calibration on the CPU)."""
     B, _, H, W = x.shape
     blob = g.weight_blob()
     T = [torch.zeros(B, c, H >> s if s >= 0 else H << -s, W >> s if s >= 0 else W << -s) for c, s in g.tensors]
@@ -56,7 +65,12 @@ def run(g, x: torch.Tensor):
             T[o['dst']][:, o['dst_coff']:o['dst_coff'] + o['cout2']] = y
         elif kind == L.OP_CONV:
             src = T[o['src']][:, o['src_coff']:o['src_coff'] + o['cin']]
-            w = _weights(blob, g.dtype, o['w_off'], o['cout'], o['k'], o['cin'])
+            if o.get('wfmt', 0) == L.WFMT_FP8:   # e4m3 input on the op's scale, e4m3 weights
+                xs = o['xscale']
+                src = (src / xs).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float() * xs
+                w = _weights_f8(blob, o['w_off'], o['cout'], o['cin'], o['s_off'])
+            else:
+                w = _weights(blob, g.dtype, o['w_off'], o['cout'], o['k'], o['cin'])
             y = _act(F.conv2d(src, w, _bias(blob, o['b_off'], o['cout']), o['s'], o['pad']), o['act'])
             T[o['dst']][:, o['dst_coff']:o['dst_coff'] + o['cout']] = y
         elif kind == L.OP_MAXPOOL:
@@ -84,4 +98,5 @@ def run(g, x: torch.Tensor):
             zs.append(torch.cat((xy, wh, y[..., 4:]), -1).view(B, -1, g.no))
         else:
             raise ValueError(f'op kind {kind}')
-    return torch.cat(zs, 1)
+    z = torch.cat(zs, 1)
+    return (z, T) if return_tensors else z

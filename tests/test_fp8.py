@@ -1,0 +1,136 @@
+"""BASELINE.json configs[4]: yolov7 640x640 with fp8 weights — the fp16 plan whose 1x1 convs run on
+OCP e4m3 weights and activations through the block-scaled fp8 MFMA (csrc/conv_f8.hip).
+
+The reference has no fp8 path; parity is anchored on (i) the e4m3 rounding itself (known answers for
+torch.float8_e4m3fn, RNE with saturation, and the GPU quantizer bit-exact against it), (ii) the oracle's
+restatement of the fp8 plan's arithmetic (oracle.yolo_ref.fp8_fused: per-channel e4m3 weights,
+per-tensor e4m3 activations, fp32 accumulation) — the CPU plan interpreter and the GPU plan against it —
+and (iii) the metric's mAP@0.5 parity of the GPU fp8 detections against the oracle's fp32 ones."""
+import math
+
+import pytest
+import torch
+
+import plan_interp
+from helpers import fresh_model, frames, oracle_net
+from oracle import metrics_ref, nms_ref, yolo_ref
+from yv7 import _lib as L
+from yv7.graph import compile_model, fp8_candidates, fp8_weight_scales
+
+
+def test_e4m3_known_answers():
+    f = yolo_ref.fp8_e4m3
+    t = torch.tensor([1.0, 0.3, 448.0, 500.0, -1000.0, 2.0 ** -9, 2.0 ** -10, 3 * 2.0 ** -10, 17.0, 19.0, 0.28125])
+    want = [1.0, 0.3125, 448.0, 448.0, -448.0, 2.0 ** -9, 0.0, 2.0 ** -8, 16.0, 20.0, 0.28125]
+    assert f(t).tolist() == want   # RNE: 2^-10 and 17 are ties to the even neighbour, 19 -> 20
+
+
+def _entries(g):
+    return [(tuple(tag), o['xscale']) for o in g.ops if o.get('wfmt', 0) == L.WFMT_FP8 for tag in o['layers']]
+
+
+def _calibrated_fp8_graph(m, x):
+    """fp8 graph with activation scales from the CPU interpreter's fp16-graph tensors (the GPU plan
+    takes them from its own fp16 forward, yv7.runtime.Plan.fp8_from_model)."""
+    g16 = compile_model(m, L.DT_F16)
+    _, T = plan_interp.run(g16, x, return_tensors=True)
+    scales = {}
+    for i in fp8_candidates(g16):
+        o = g16.ops[i]
+        amax = float(T[o['src']][:, o['src_coff']:o['src_coff'] + o['cin']].abs().max())
+        scales[i] = 2.0 ** math.ceil(math.log2(amax / 448.0)) if amax > 0 else 1.0
+    return g16, compile_model(m, L.DT_F16, fp8=scales)
+
+
+def test_fp8_graph_packing():
+    m = fresh_model('yolov7')
+    x = frames(1, 64, 64, seed=2)
+    g16, g8 = _calibrated_fp8_graph(m, x)
+    f8 = [o for o in g8.ops if o.get('wfmt', 0) == L.WFMT_FP8]
+    assert len(f8) == len(fp8_candidates(g16)) > 30
+    assert all(o['kind'] == L.OP_CONV and o['k'] == 1 for o in f8)
+    assert not any(o.get('wfmt', 0) for o in g8.ops if o['kind'] == L.OP_DETECT)
+    for o in f8:
+        xs = o['xscale']
+        assert xs > 0 and math.log2(xs) == round(math.log2(xs))       # power of two
+    # one op's packed e4m3 weights and scales == the per-channel quantization of the fused weights
+    blob = g8.weight_blob()
+    o = f8[3]
+    (layer, sub), = o['layers'][:1] if len(o['layers']) == 1 else [o['layers'][0]]
+    conv = m.model[layer] if sub is None else getattr(m.model[layer], f'cv{sub}')
+    w, _ = conv.fused_weight_bias()
+    wk = w.reshape(w.shape[0], -1)[:o['cout']]
+    ws = fp8_weight_scales(wk)
+    got = plan_interp._weights_f8(blob, o['w_off'], o['cout'], o['cin'], o['s_off']).reshape(o['cout'], -1)
+    want = yolo_ref.fp8_e4m3(wk / ws[:, None]) * ws[:, None]
+    assert torch.equal(got[:wk.shape[0], :wk.shape[1]], want)
+
+
+@pytest.mark.parametrize('name', ['yolov7', 'yolov7-tiny'])
+def test_fp8_plan_semantics_vs_oracle_emulation(name):
+    """The compiled fp8 plan run op by op on the CPU equals the oracle's fp8 restatement (same
+    quantization points and scales) up to fp32 summation order and fp16 weight storage."""
+    m = fresh_model(name)
+    x = frames(1, 128, 128, seed=3)
+    _, g8 = _calibrated_fp8_graph(m, x)
+    net, fused = oracle_net(name)
+    emu = yolo_ref.half_weights(yolo_ref.fp8_fused(fused, _entries(g8)))
+    with torch.no_grad():
+        got = plan_interp.run(g8, x)
+        want = yolo_ref.forward(net, emu, x)[0]
+    rel = ((got - want).pow(2).mean().sqrt() / want.pow(2).mean().sqrt()).item()
+    assert rel < 2e-3, rel
+    gt = [metrics_ref.dets_as_labels(d) for d in nms_ref.non_max_suppression(want, 0.25, 0.45)]
+    m50, _ = metrics_ref.map_from_lists(nms_ref.non_max_suppression(got, 0.25, 0.45), gt)
+    assert m50 >= 0.98, m50
+
+
+# ------------------------------------------------------------------------------------------ GPU
+def _gpu_fp8_plan(name, calib):
+    from yv7.runtime import Plan
+    m = fresh_model(name).cuda().half()
+    return Plan.fp8_from_model(m, 'cuda:0', calib=calib)
+
+
+@pytest.mark.gpu
+def test_gpu_fp8_quantizer_bit_exact():
+    """The GPU quantizer (v_cvt_pk_fp8_f32 after a power-of-two scale and +-448 clamp) writes exactly
+    torch.float8_e4m3fn's bytes for the fp16 input it read (checked on the last fp8 op of a forward)."""
+    B, H, W = 2, 128, 160
+    x = frames(B, H, W, seed=5)
+    plan = _gpu_fp8_plan('yolov7', x)
+    z = torch.empty(B, plan.num_rows(H, W), plan.no, device='cuda:0')
+    plan.forward_into(x.cuda().half(), z)
+    torch.cuda.synchronize()
+    o = [o for o in plan.graph.ops if o.get('wfmt', 0) == L.WFMT_FP8][-1]
+    src = plan.tensor_view(o['src'], B, H, W)[..., o['src_coff']:o['src_coff'] + o['cin']].float().cpu()
+    M, cin = src.numel() // o['cin'], o['cin']
+    kp = (cin + 127) // 128 * 128
+    want = torch.zeros(M, kp, dtype=torch.uint8)
+    want[:, :cin] = (src.reshape(M, cin) / o['xscale']).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+    got = plan.f8_scratch(B, H, W)[:M * kp].view(M, kp).cpu()
+    assert torch.equal(got, want), int((got != want).sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['yolov7', 'yolov7-tiny'])
+def test_gpu_fp8_map_parity(name):
+    """configs[4] parity: mAP@0.5 of the GPU fp8 plan's detections against the oracle's fp32 detections
+    (the metric's ground truth) and against the oracle's restatement of the fp8 arithmetic on the same
+    scales (fp16 storage elsewhere); conf 0.25 / iou 0.45, 2 frames at 640."""
+    x = frames(2, 640, 640, seed=8)
+    plan = _gpu_fp8_plan(name, None)
+    z, _ = plan.forward(x.cuda().half(), want_raw=False)
+    pred = [d.cpu() for d in nms_ref.non_max_suppression(z.cpu(), 0.25, 0.45)]
+    net, fused = oracle_net(name)
+    with torch.no_grad():
+        zr, _ = yolo_ref.forward(net, fused, x)
+        ze, _ = yolo_ref.forward(net, yolo_ref.fp8_fused(fused, _entries(plan.graph)), x, half_storage=True)
+    gt = [metrics_ref.dets_as_labels(d) for d in nms_ref.non_max_suppression(zr, 0.25, 0.45)]
+    ge = [metrics_ref.dets_as_labels(d) for d in nms_ref.non_max_suppression(ze, 0.25, 0.45)]
+    m32, _ = metrics_ref.map_from_lists(pred, gt)
+    memu, _ = metrics_ref.map_from_lists(pred, ge)
+    emu32, _ = metrics_ref.map_from_lists([d for d in nms_ref.non_max_suppression(ze, 0.25, 0.45)], gt)
+    print(f'\n{name} fp8: mAP@0.5 vs fp32 oracle {m32:.4f} (oracle fp8 restatement vs fp32: {emu32:.4f}), '
+          f'vs fp8 restatement {memu:.4f}; dets {[len(d) for d in pred]}')
+    assert m32 >= 0.5 and memu >= 0.5

@@ -1,0 +1,284 @@
+// fp8 (OCP e4m3) 1x1 convolution for gfx950 — BASELINE.json configs[4]: "yolov7 640x640 fp8 weights
+// (CDNA4 fp8 MFMA for 1x1 convs)".  Replaces Conv.fuseforward (models/common.py:110-111) for the 1x1
+// layers of an fp16 plan whose ops are marked wfmt = YV7_WFMT_FP8.
+//
+// Two launches per layer:
+//  * quant_f8_kernel: the layer's fp16 NHWC input slice (bordered workspace tensor) -> a dense fp8 copy
+//    [M][kp] (kp = cin rounded up to 128, zero-filled), x8 = e4m3(clamp(x * qscale, +-448)) with a
+//    power-of-two per-tensor qscale from calibration (exact in fp32, so the only rounding is e4m3's RNE,
+//    v_cvt_pk_fp8_f32 — OCP e4m3fn on gfx950);
+//  * conv_f8_kernel: persistent LDS-DMA ring GEMM on the block-scaled MFMA
+//    v_mfma_scale_f32_16x16x128_f8f6f4 (e4m3 x e4m3, unit block scales: 2x the fp16 MFMA rate).  A K
+//    step is 128 fp8 = 128 bytes per tile row — the same LDS image (8 x 16-byte chunks, XOR swizzle)
+//    the fp16 ring uses for 64 halves, so fills are the same 1 KiB DMA pieces.  Each lane feeds the
+//    MFMA the two chunks (2g, 2g+1) of its row (lane group g = lane >> 4): A (weights) and B
+//    (activations) use the same (lane, element) -> k assignment, so the sum over k is exact whatever
+//    order the instruction assigns inside a group.
+//    Epilogue: acc * (xscale * wscale[c]) + bias[c] -> activation -> fp16, 16-byte NHWC stores into the
+//    destination channel slice (permlane16 pairing as in the fp16 persistent ring).
+#include "yv7_kernels.h"
+
+namespace yv7 {
+
+namespace {
+
+typedef int v8i __attribute__((ext_vector_type(8)));
+constexpr int ROWB8 = 128;   // LDS bytes per tile row per K step (128 fp8)
+
+__device__ __forceinline__ void dma16_f8(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t vo, uint32_t so) {
+  __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, vo, so, 0, 0);
+}
+
+__device__ __forceinline__ int swz8(int row, int chunk) { return chunk ^ (row & 7); }
+
+int cu_count() {
+  static const int n = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  return n;
+}
+
+// ---- quantization: bordered fp16 NHWC slice -> dense e4m3 [M][kp]
+__global__ __launch_bounds__(256) void quant_f8_kernel(const _Float16* __restrict__ x, int B, int H, int W, int xc,
+                                                       int xoff, int cin, int kp, float qscale,
+                                                       uint8_t* __restrict__ y) {
+  const int cpp = kp / 16;                 // 16-channel chunks per pixel
+  const int total = B * H * W * cpp;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < total; i += gridDim.x * 256) {
+    const int pix = i / cpp, c = (i - pix * cpp) * 16;
+    const int t = pix / W, w = pix - t * W;
+    const int b = t / H, h = t - b * H;
+    const _Float16* src = x + pix_index(b, h, w, H, W) * xc + xoff + c;
+    u4 lo = {0u, 0u, 0u, 0u}, hi = {0u, 0u, 0u, 0u};
+    if (c < cin) lo = *reinterpret_cast<const u4*>(src);
+    if (c + 8 < cin) hi = *reinterpret_cast<const u4*>(src + 8);
+    const _Float16* a = reinterpret_cast<const _Float16*>(&lo);
+    const _Float16* bb = reinterpret_cast<const _Float16*>(&hi);
+    float v[16];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      v[e] = __builtin_fminf(__builtin_fmaxf((float)a[e] * qscale, -448.0f), 448.0f);
+      v[e + 8] = __builtin_fminf(__builtin_fmaxf((float)bb[e] * qscale, -448.0f), 448.0f);
+    }
+    u4 o;
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      int r = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * d], v[4 * d + 1], 0, false);
+      r = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * d + 2], v[4 * d + 3], r, true);
+      o[d] = (uint32_t)r;
+    }
+    *reinterpret_cast<u4*>(y + (size_t)pix * kp + c) = o;
+  }
+}
+
+// ---- persistent fp8 ring GEMM (1x1): M pixels x N = cout x K = kp
+template <int BM, int BN, int WM, int WN, int STAGES, int ACT>
+__global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * ROWB8 <= 76 * 1024) ? 2 : 1) void conv_f8_kernel(
+    const F8ConvParams p) {
+  constexpr int NW = WM * WN, NTH = 64 * NW;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int RA = BM / 8 / NW, RB = BN / 8 / NW;   // 1 KiB DMA pieces (8 rows) per wave per stage
+  static_assert(RA * 8 * NW == BM && RB * 8 * NW == BN, "tile rows must split into 8-row pieces per wave");
+  static_assert(TN % 2 == 0, "the epilogue pairs 16-channel groups");
+  static_assert(STAGES >= 2 && STAGES <= 3, "counted waits cover one stage in flight");
+  constexpr int PER = RA + RB;
+  constexpr int NST = TM * TN / 2;
+  constexpr int STAGE = (BM + BN) * ROWB8;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + 8192];
+  float* bias_l = reinterpret_cast<float*>(smem + STAGES * STAGE);
+  float* scale_l = bias_l + 1024;
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, li = lane & 15;
+  const int lr = lane >> 3;                 // row within the 8-row DMA piece
+  const int c = (lane & 7) ^ lr;            // source chunk this lane fetches (slot = lane & 7)
+
+  const int nN = (p.cout + BN - 1) / BN;
+  const int T = ((p.M + BM - 1) / BM) * nN;
+  const int G = gridDim.x;
+  const int nk = p.kp / 128;
+  const int ntl = (T - (int)blockIdx.x + G - 1) / G;
+  const int nsteps = ntl * nk;
+
+  const auto xr = make_rsrc(p.x8, (uint32_t)((size_t)p.M * p.kp));
+  const auto wr = make_rsrc(p.w8, p.wbytes);
+  const auto yr = make_rsrc(p.y, 0x7fffffffu);
+
+  for (int i = tid; i < p.cout; i += NTH) {
+    bias_l[i] = p.bias[i];
+    scale_l[i] = p.xscale * p.wscale[i];
+  }
+
+  uint32_t a_off[RA], b_off[RB];
+  int ig = 0, it = 0, ikt = 0;
+  auto issue_next = [&]() {
+    if (ikt == 0) {
+      const int t = blockIdx.x + it * G;
+      const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+#pragma unroll
+      for (int j = 0; j < RA; ++j) {
+        const int m = m0 + (j * NW + wave) * 8 + lr;
+        a_off[j] = m < p.M ? (uint32_t)m * p.kp + c * 16 : 0x80000000u;
+      }
+#pragma unroll
+      for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)((n0 + (j * NW + wave) * 8 + lr) * p.kp + c * 16);
+    }
+    unsigned char* As = smem + (ig % STAGES) * STAGE;   // weights (MFMA A operand), BN rows
+    unsigned char* Bs = As + BN * ROWB8;                 // activations (MFMA B operand), BM rows
+    const uint32_t so = (uint32_t)ikt * 128;
+#pragma unroll
+    for (int j = 0; j < RB; ++j) dma16_f8(wr, As + (j * NW + wave) * 8 * ROWB8, b_off[j], so);
+#pragma unroll
+    for (int j = 0; j < RA; ++j) dma16_f8(xr, Bs + (j * NW + wave) * 8 * ROWB8, a_off[j], so);
+    ++ig;
+    if (++ikt == nk) { ikt = 0; ++it; }
+  };
+
+  f4 acc[TN][TM];
+  int cm0 = 0, cn0 = 0;
+  auto init_tile = [&](int i) {
+    const int t = blockIdx.x + i * G;
+    cm0 = (t / nN) * BM;
+    cn0 = (t % nN) * BN;
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) acc[j][ii] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  };
+  const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
+  auto epilogue = [&]() {
+    float sc[TN][4], bi[TN][4];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = cn0 + wn * WTN + j * 16 + g * 4 + e;
+        sc[j][e] = col < p.cout ? scale_l[col] : 0.0f;
+        bi[j][e] = col < p.cout ? bias_l[col] : 0.0f;
+      }
+    const int hw = p.H * p.W;
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii) {
+      const int m = cm0 + wm * WTM + ii * 16 + li;
+      const int mm = m < p.M ? m : 0;
+      const int b = mm / hw, r = mm - b * hw, h = r / p.W, w = r - h * p.W;
+      const uint32_t yo = (uint32_t)((pix_index(b, h, w, p.H, p.W) * p.yc + p.yoff) * 2);
+#pragma unroll
+      for (int mp = 0; mp < TN / 2; ++mp) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        h4 va, vb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          va[e] = (_Float16)act_t<ACT>(__builtin_fmaf(acc[2 * mp][ii][e], sc[2 * mp][e], bi[2 * mp][e]));
+          vb[e] = (_Float16)act_t<ACT>(__builtin_fmaf(acc[2 * mp + 1][ii][e], sc[2 * mp + 1][e], bi[2 * mp + 1][e]));
+        }
+        const u2 a = __builtin_bit_cast(u2, va), bq = __builtin_bit_cast(u2, vb);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], bq[0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], bq[1], false, false);
+        const u4 v = {s0[0], s1[0], s0[1], s1[1]};
+        const int n = cn0 + wn * WTN + mp * 32 + (int)lane_ch;
+        const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
+        __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+      }
+    }
+  };
+
+#pragma unroll
+  for (int s0 = 0; s0 < STAGES - 1; ++s0)
+    if (ig < nsteps) issue_next();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bias / scale LDS writes of this wave
+  __builtin_amdgcn_s_barrier();
+  init_tile(0);
+
+  int ci = 0, ckt = 0;
+  for (int gs = 0; gs < nsteps; ++gs) {
+    // stage gs has landed once at most `younger` vector-memory ops of this wave are outstanding:
+    // the next stage's pieces (if issued) and, right after a tile boundary, the epilogue's stores
+    const int ndma = min(STAGES - 2, nsteps - 1 - gs);
+    const bool st = ci > 0 && ckt <= STAGES - 2;
+    const int younger = ndma * PER + (st ? NST : 0);
+    if (younger == 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    else if (younger == PER) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+    else if (younger == NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NST) : "memory");
+    else if (younger == PER + NST) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + NST) : "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (ig < nsteps) issue_next();   // refills the slot every wave finished reading at step gs-1
+    const unsigned char* As = smem + (gs % STAGES) * STAGE;
+    const unsigned char* Bs = As + BN * ROWB8;
+    v8i wa[TN], xb[TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wn * WTN + j * 16 + li;
+      const u4 q0 = *reinterpret_cast<const u4*>(As + row * ROWB8 + swz8(row, 2 * g) * 16);
+      const u4 q1 = *reinterpret_cast<const u4*>(As + row * ROWB8 + swz8(row, 2 * g + 1) * 16);
+      wa[j] = v8i{(int)q0[0], (int)q0[1], (int)q0[2], (int)q0[3], (int)q1[0], (int)q1[1], (int)q1[2], (int)q1[3]};
+    }
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii) {
+      const int row = wm * WTM + ii * 16 + li;
+      const u4 q0 = *reinterpret_cast<const u4*>(Bs + row * ROWB8 + swz8(row, 2 * g) * 16);
+      const u4 q1 = *reinterpret_cast<const u4*>(Bs + row * ROWB8 + swz8(row, 2 * g + 1) * 16);
+      xb[ii] = v8i{(int)q0[0], (int)q0[1], (int)q0[2], (int)q0[3], (int)q1[0], (int)q1[1], (int)q1[2], (int)q1[3]};
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii)
+        // cbsz = blgp = 0: both operands e4m3; scale operands 127 = 2^0 (E8M0)
+        acc[j][ii] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[j], xb[ii], acc[j][ii], 0, 0, 0, 127, 0, 127);
+    __builtin_amdgcn_s_setprio(0);
+    if (++ckt == nk) {
+      epilogue();
+      ckt = 0;
+      if (++ci < ntl) init_tile(ci);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <int BM, int BN, int WM, int WN, int STAGES>
+hipError_t launch_f8(const F8ConvParams& p, int occ, hipStream_t st) {
+  const long T = (long)((p.M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
+  const long cap = (long)cu_count() * occ;
+  const int grid = (int)(T < cap ? T : cap);
+  const dim3 blk(64 * WM * WN);
+  if (p.act == 1) hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 1>), dim3(grid), blk, 0, st, p);
+  else if (p.act == 2) hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 2>), dim3(grid), blk, 0, st, p);
+  else hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 0>), dim3(grid), blk, 0, st, p);
+  return hipGetLastError();
+}
+
+}  // namespace
+
+hipError_t launch_quant_f8(const void* x, int B, int H, int W, int xc, int xoff, int cin, int kp, float qscale,
+                           void* y8, hipStream_t st) {
+  if (cin % 8 || kp % 128 || kp < cin || xoff % 8 || xc % 8) return hipErrorInvalidValue;
+  const size_t work = (size_t)B * H * W * (kp / 16);
+  size_t g = (work + 255) / 256;
+  if (g > 256 * 16) g = 256 * 16;
+  hipLaunchKernelGGL(quant_f8_kernel, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st,
+                     reinterpret_cast<const _Float16*>(x), B, H, W, xc, xoff, cin, kp, qscale,
+                     reinterpret_cast<uint8_t*>(y8));
+  return hipGetLastError();
+}
+
+hipError_t launch_conv_f8(const F8ConvParams& p, hipStream_t st) {
+  if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || p.kp % 128 || p.M <= 0 ||
+      (size_t)p.M * p.kp >= ((size_t)1 << 31))
+    return hipErrorInvalidValue;
+  // 128 x 128 tiles, two 4-wave blocks per CU (a 256 x 256 tile's 32 fragment registers of 32 fp8 each
+  // per operand do not fit beside its 128 accumulators: it spills)
+  return launch_f8<128, 128, 2, 2, 2>(p, 2, st);
+}
+
+}  // namespace yv7

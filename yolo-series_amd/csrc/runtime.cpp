@@ -94,7 +94,12 @@ int check_hw(const yv7_plan* p, int B, int H, int W) {
   return 0;
 }
 
-int kpad_of(const yv7_op_desc& o) { return (o.k * o.k * o.cin + 63) / 64 * 64; }
+// K padding of a conv's packed weights: 64 in the plan dtype, 128 for fp8 (one MFMA K step)
+int kpad_of(const yv7_op_desc& o) {
+  if (o.kind == YV7_OP_CONV && o.wfmt == YV7_WFMT_FP8) return (o.cin + 127) / 128 * 128;
+  return (o.k * o.k * o.cin + 63) / 64 * 64;
+}
+bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7_WFMT_FP8; }
 
 // Geometry / operand fields of a CONV or DETECT op's kernel parameters (pointers into the workspace
 // are filled by the caller).
@@ -130,21 +135,28 @@ yv7::ConvParams conv_params(const yv7_plan* p, const yv7_op_desc& o, int B, int 
 struct SplitScratch {
   size_t part_off = 0, part_bytes = 0, cnt_off = 0;
   int cnt_n = 0;
+  size_t f8_off = 0, f8_bytes = 0;   // dense e4m3 copy of an FP8 op's input (the largest one)
   size_t end = 0;
 };
 
 SplitScratch split_scratch(const yv7_plan* p, int B, int H, int W, size_t tensors_end) {
   SplitScratch s;
-  if (p->dtype == YV7_DT_F16)
-    for (const auto& o : p->ops)
-      if (o.kind == YV7_OP_CONV) {
+  if (p->dtype == YV7_DT_F16) {
+    for (const auto& o : p->ops) {
+      if (o.kind == YV7_OP_CONV && !is_f8(o)) {
         const yv7::ConvParams c = conv_params(p, o, B, H, W);
         s.part_bytes = std::max(s.part_bytes, yv7::conv_splitk_part_bytes(c));
         s.cnt_n = std::max(s.cnt_n, yv7::conv_splitk_tiles(c));
+      } else if (is_f8(o)) {
+        const int sh = p->tensors[o.src].shift;
+        s.f8_bytes = std::max(s.f8_bytes, (size_t)B * (H >> sh) * (W >> sh) * kpad_of(o));
       }
+    }
+  }
   s.part_off = tensors_end;
   s.cnt_off = align256(s.part_off + s.part_bytes);
-  s.end = align256(s.cnt_off + (size_t)s.cnt_n * 4);
+  s.f8_off = align256(s.cnt_off + (size_t)s.cnt_n * 4);
+  s.end = align256(s.f8_off + s.f8_bytes);
   return s;
 }
 
@@ -178,7 +190,14 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
     if (o.kind == YV7_OP_CONV || o.kind == YV7_OP_DETECT) {
       if (o.cin % vec || (o.kind == YV7_OP_CONV && o.cout % vec))
         return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " channels not a multiple of the vector");
-      const size_t wb = (size_t)((o.cout + 31) / 32 * 32) * kpad_of(o) * elem_size(d->dtype);
+      if (o.kind == YV7_OP_CONV && o.wfmt != YV7_WFMT_PLAN) {
+        if (o.wfmt != YV7_WFMT_FP8 || d->dtype != YV7_DT_F16 || o.k != 1 || o.s != 1 || o.pad != 0 ||
+            o.cout > 1024 || !(o.xscale > 0.0f) || o.xscale > 1e30f || o.s_off < 0 ||
+            (size_t)o.s_off + sizeof(float) * o.cout > nbytes)
+          return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) +
+                                     " bad fp8 conv (fp16 plans, 1x1 stride 1, cout <= 1024, xscale > 0, scales in blob)");
+      }
+      const size_t wb = (size_t)((o.cout + 31) / 32 * 32) * kpad_of(o) * (is_f8(o) ? 1 : elem_size(d->dtype));
       if (o.w_off < 0 || o.b_off < 0 || (size_t)o.w_off + wb > nbytes ||
           (size_t)o.b_off + sizeof(float) * o.cout > nbytes)
         return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " weight range outside blob");
@@ -418,6 +437,30 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
           c.y = wsb + off[o.dst];
           c.yc = to.channels;
           c.yoff = o.dst_coff;
+          if (is_f8(o)) {
+            // quantize the input slice to the dense e4m3 staging buffer, then the fp8 GEMM
+            unsigned char* x8 = wsb + scr.f8_off;
+            e = yv7::launch_quant_f8(c.x, B, c.H, c.W, c.xc, c.xoff, o.cin, c.kpad, 1.0f / o.xscale, x8, st);
+            if (e != hipSuccess) return hip_fail(e, "yv7_forward fp8 quantize");
+            yv7::F8ConvParams f;
+            f.x8 = x8;
+            f.y = c.y;
+            f.w8 = c.w;
+            f.bias = c.bias;
+            f.wscale = reinterpret_cast<const float*>(wb + o.s_off);
+            f.xscale = o.xscale;
+            f.wbytes = (uint32_t)((size_t)((o.cout + 31) / 32 * 32) * c.kpad);
+            f.M = c.M;
+            f.kp = c.kpad;
+            f.cout = o.cout;
+            f.H = c.Ho;
+            f.W = c.Wo;
+            f.yc = c.yc;
+            f.yoff = c.yoff;
+            f.act = o.act;
+            e = yv7::launch_conv_f8(f, st);
+            break;
+          }
           e = yv7::launch_conv(p->dtype, c, false, st);
         } else {
           c.z = z;
@@ -511,6 +554,17 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   if (rowbest && !rowbest_fused &&
       (e = yv7::launch_row_best(z, B, nrows, p->no, rowbest, st)) != hipSuccess)
     return hip_fail(e, "yv7_forward row scores");
+  return 0;
+}
+
+int yv7_f8_scratch_info(const yv7_plan* p, int B, int H, int W, int64_t* offset, int64_t* bytes) {
+  if (!p || !offset || !bytes) return fail(YV7_E_ARG, "yv7_f8_scratch_info");
+  if (int rc = check_hw(p, B, H, W)) return rc;
+  size_t total = 0;
+  tensor_offsets(p, B, H, W, &total);
+  const SplitScratch s = split_scratch(p, B, H, W, total);
+  *offset = (int64_t)s.f8_off;
+  *bytes = (int64_t)s.f8_bytes;
   return 0;
 }
 

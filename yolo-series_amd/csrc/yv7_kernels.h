@@ -84,6 +84,22 @@ struct ConvParams {
 size_t conv_splitk_part_bytes(const ConvParams& p);
 int conv_splitk_tiles(const ConvParams& p);
 
+// fp8 1x1 conv (conv_f8.hip): dense e4m3 activations [M][kp] x e4m3 weights [cout_pad32][kp], fp32
+// per-channel weight scales and a per-tensor activation scale applied in the epilogue.
+struct F8ConvParams {
+  const void* x8;       // dense e4m3 input [M][kp] (written by launch_quant_f8)
+  void* y;              // bordered NHWC fp16 output tensor
+  const void* w8;       // e4m3 weights [cout_pad32][kp]
+  const float* bias;    // [cout]
+  const float* wscale;  // [cout] per-channel weight scales
+  float xscale;         // activation scale: x ~ e4m3 value * xscale
+  uint32_t wbytes;      // byte size of w8 (buffer range)
+  int M, kp, cout, H, W, yc, yoff, act;   // H, W: output (= input) interior size
+};
+hipError_t launch_quant_f8(const void* x, int B, int H, int W, int xc, int xoff, int cin, int kp, float qscale,
+                           void* y8, hipStream_t st);
+hipError_t launch_conv_f8(const F8ConvParams& p, hipStream_t st);
+
 // Fused stem: image -> conv A (3 -> 32, 3x3, stride sa) -> conv B (32 -> 64, 3x3, stride 2).
 struct StemParams {
   const void* x;        // [B,3,H,W] image (fp16 or fp32)

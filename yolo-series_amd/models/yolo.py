@@ -305,13 +305,23 @@ class Model(nn.Module):
         self._plans = {}
         return super().load_state_dict(*args, **kwargs)
 
+    def fp8(self, calib=None):
+        """BASELINE configs[4]: half() with the 1x1 convs on OCP e4m3 weights and activations (the
+        block-scaled fp8 MFMA); `calib`: [B,3,H,W] frames in [0,1] that set the activation scales
+        (default: seeded synthetic frames) — yv7.runtime.Plan.fp8_from_model.  .float() leaves it."""
+        self.half()
+        self._fp8 = (calib,)
+        self._plans = {}
+        return self
+
     def _plan(self, device):
         dtype = next(self.parameters()).dtype
-        key = (str(device), dtype)
+        fp8 = getattr(self, '_fp8', None) if dtype == torch.float16 else None
+        key = (str(device), 'fp8' if fp8 else dtype)
         p = self._plans.get(key)
         if p is None:
             from yv7.runtime import Plan
-            p = Plan.from_model(self, device=device, dtype=dtype)
+            p = Plan.from_model(self, device=device, dtype='fp8' if fp8 else dtype, calib=fp8[0] if fp8 else None)
             self._plans[key] = p
         return p
 

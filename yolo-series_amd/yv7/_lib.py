@@ -13,11 +13,12 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libyv7.so')
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 BORDER = 1          # zero frame around every workspace tensor (YV7_BORDER)
 DT_F32, DT_F16 = 0, 1
 ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
 OP_INPUT, OP_CONV, OP_MAXPOOL, OP_UPSAMPLE, OP_COPY, OP_DETECT, OP_STEM = 0, 1, 2, 3, 4, 5, 6
+WFMT_PLAN, WFMT_FP8 = 0, 1
 
 
 class TensorDesc(ctypes.Structure):
@@ -32,7 +33,8 @@ class OpDesc(ctypes.Structure):
                 ('level', ctypes.c_int32),
                 ('w_off', ctypes.c_int64), ('b_off', ctypes.c_int64),
                 ('cout2', ctypes.c_int32), ('act2', ctypes.c_int32),
-                ('w2_off', ctypes.c_int64), ('b2_off', ctypes.c_int64)]
+                ('w2_off', ctypes.c_int64), ('b2_off', ctypes.c_int64),
+                ('wfmt', ctypes.c_int32), ('xscale', ctypes.c_float), ('s_off', ctypes.c_int64)]
 
 
 class NetDesc(ctypes.Structure):
@@ -58,6 +60,7 @@ SIGNATURES = {
     'yv7_profile_enable': (_i, [_vp, _i]),
     'yv7_profile_read': (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_float)]),
     'yv7_tensor_info': (_i, [_vp, _i, _i, _i, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
+    'yv7_f8_scratch_info': (_i, [_vp, _i, _i, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),
     'yv7_nms_workspace_bytes': (_sz, [_i, _i, _i, _i, _i]),
     'yv7_nms': (_i, [_vp, _vp, _i, _i, _i, _f, _f, _i, _i, _vp, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     'yv7_end2end_workspace_bytes': (_sz, [_i, _i, _i, _i]),

@@ -102,6 +102,40 @@ def _pack_conv(g: Graph, w: torch.Tensor, b: torch.Tensor, cin_pad: int):
     return w_off, b_off
 
 
+def _pack_conv_f8(g: Graph, w: torch.Tensor, b: torch.Tensor, cin_pad: int):
+    """fp32 1x1 W [cout, cin, 1, 1] -> OCP e4m3 [cout_pad32][cin padded to 128] with per-output-channel
+    scales wscale = amax / 448 (W ~ e4m3(W / wscale) * wscale, round to nearest even); bias fp32."""
+    cout, cin = w.shape[:2]
+    wk = w.reshape(cout, cin).float()
+    ws = fp8_weight_scales(wk)
+    q = (wk / ws[:, None]).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
+    kp, cpad = _rup(cin_pad, 128), _rup(cout, 32)
+    wp = torch.zeros(cpad, kp, dtype=torch.uint8)
+    wp[:cout, :cin] = q
+    bp = torch.zeros(cpad, dtype=torch.float32)
+    bp[:cout] = b
+    sp = torch.zeros(cpad, dtype=torch.float32)
+    sp[:cout] = ws
+    return g.add_blob(wp), g.add_blob(bp), g.add_blob(sp)
+
+
+def fp8_weight_scales(wk: torch.Tensor) -> torch.Tensor:
+    """Per-output-channel e4m3 scales of a [cout, K] weight matrix: amax / 448 (1 for an all-zero row)."""
+    amax = wk.abs().amax(1)
+    return torch.where(amax > 0, amax / 448.0, torch.ones_like(amax))
+
+
+def fp8_eligible(g: Graph, o: dict) -> bool:
+    """CONV ops an fp8 plan runs in e4m3: 1x1 stride-1 convs of an fp16 plan (the Detect head stays fp16)."""
+    return (g.dtype == L.DT_F16 and o['kind'] == L.OP_CONV and o['k'] == 1 and o['s'] == 1 and o['pad'] == 0
+            and o['cout'] <= 1024)
+
+
+def fp8_candidates(g: Graph):
+    """Op indices of `g` that compile_model(..., fp8={index: xscale}) can mark FP8."""
+    return [i for i, o in enumerate(g.ops) if fp8_eligible(g, o)]
+
+
 def _live_layers(layers, nl):
     """Layers whose output reaches the Detect head (drops IAuxDetect's auxiliary branch)."""
     n = len(layers)
@@ -141,7 +175,9 @@ def _stem_candidate(layers, dtype):
     return True
 
 
-def compile_model(model, dtype: int) -> Graph:
+def compile_model(model, dtype: int, fp8=None) -> Graph:
+    """fp8: {op index: activation scale} — those ops (fp8_candidates of the same model and dtype) are
+    packed as YV7_WFMT_FP8 (e4m3 weights + scales); the op list is otherwise identical."""
     layers = list(model.model)
     det = layers[-1]
     if not isinstance(det, Detect):
@@ -236,14 +272,15 @@ def compile_model(model, dtype: int) -> Graph:
             loc[i] = (g.add_tensor(_rup(ch[i], V), shift[i]), 0)
         return loc[i]
 
-    def conv_op(src, dst, w, b, k, s, pad, act):
-        # weights are packed after the sibling-merge pass (_merge_siblings), so they ride along unpacked
+    def conv_op(src, dst, w, b, k, s, pad, act, tag):
+        # weights are packed after the sibling-merge pass (_merge_siblings), so they ride along unpacked;
+        # tag = (layer, SPPCSPC cv index or None) names the reference conv(s) an op computes
         (ts, so, cs), (td, do) = src, dst
         cin_pad = _rup(cs, V)
         if cin_pad != cs and g.tensors[ts][0] < so + cin_pad:
             raise ValueError('channel padding would read outside the source tensor')
         g.ops.append(dict(kind=L.OP_CONV, src=ts, src_coff=so, cin=cin_pad, dst=td, dst_coff=do, cout=w.shape[0],
-                          k=k, s=s, pad=pad, act=act, _w=w, _b=b))
+                          k=k, s=s, pad=pad, act=act, _w=w, _b=b, layers=[tag]))
 
     for m in layers:
         i = m.i
@@ -266,7 +303,8 @@ def compile_model(model, dtype: int) -> Graph:
             c = m.conv if isinstance(m, Conv) else (m.rbr_reparam if hasattr(m, 'rbr_reparam') else m.rbr_dense[0])
             if c.groups != 1 or c.dilation[0] != 1:
                 raise NotImplementedError('grouped / dilated conv')
-            conv_op(src_of(i, m.f), out_of(i), w, b, c.kernel_size[0], c.stride[0], c.padding[0], _act_code(m.act))
+            conv_op(src_of(i, m.f), out_of(i), w, b, c.kernel_size[0], c.stride[0], c.padding[0], _act_code(m.act),
+                    (i, None))
         elif isinstance(m, SPPCSPC):
             src = src_of(i, m.f)
             c_ = m.cv1.conv.out_channels
@@ -279,14 +317,15 @@ def compile_model(model, dtype: int) -> Graph:
             if c_ % V:
                 raise NotImplementedError('SPPCSPC hidden width must be a multiple of the vector width')
 
-            def cv(mod, a, d):
+            def cv(j, a, d):
+                mod = getattr(m, f'cv{j}')
                 w, b = mod.fused_weight_bias()
                 k = mod.conv.kernel_size[0]
-                conv_op(a, d, w, b, k, 1, k // 2, _act_code(mod.act))
+                conv_op(a, d, w, b, k, 1, k // 2, _act_code(mod.act), (i, j))
 
-            cv(m.cv1, src, (t1, 0))
-            cv(m.cv3, (t1, 0, c_), (t3, 0))
-            cv(m.cv4, (t3, 0, c_), (cat1, 0))
+            cv(1, src, (t1, 0))
+            cv(3, (t1, 0, c_), (t3, 0))
+            cv(4, (t3, 0, c_), (cat1, 0))
             ks = [p.kernel_size for p in m.m]
             if ks == [5, 9, 13]:  # cascade: pool9 = pool5(pool5), pool13 = pool5(pool9)
                 for q in range(3):
@@ -296,10 +335,10 @@ def compile_model(model, dtype: int) -> Graph:
                 for q, k in enumerate(ks):
                     g.ops.append(dict(kind=L.OP_MAXPOOL, src=cat1, src_coff=0, dst=cat1, dst_coff=(q + 1) * c_,
                                       cout=c_, k=k, s=1, pad=k // 2))
-            cv(m.cv5, (cat1, 0, 4 * c_), (t5, 0))
-            cv(m.cv6, (t5, 0, c_), (cat2, 0))
-            cv(m.cv2, src, (cat2, c_))
-            cv(m.cv7, (cat2, 0, 2 * c_), out_of(i))
+            cv(5, (cat1, 0, 4 * c_), (t5, 0))
+            cv(6, (t5, 0, c_), (cat2, 0))
+            cv(2, src, (cat2, c_))
+            cv(7, (cat2, 0, 2 * c_), out_of(i))
         elif isinstance(m, (MP, SP)):
             (ts, so, cs), (td, do) = src_of(i, m.f), out_of(i)
             p = m.m
@@ -331,9 +370,17 @@ def compile_model(model, dtype: int) -> Graph:
                                   k=1, s=1, pad=0, level=lvl, w_off=w_off, b_off=b_off))
     if os.environ.get('YV7_NO_MERGE') != '1':
         _merge_siblings(g)
-    for o in g.ops:
+    fp8 = fp8 or {}
+    for idx, o in enumerate(g.ops):
         if '_w' in o:
-            o['w_off'], o['b_off'] = _pack_conv(g, o.pop('_w'), o.pop('_b'), o['cin'])
+            w, b = o.pop('_w'), o.pop('_b')
+            if idx in fp8:
+                if not fp8_eligible(g, o):
+                    raise ValueError(f'op {idx} cannot run in fp8 (fp16 plans, 1x1 stride-1 convs only)')
+                o['w_off'], o['b_off'], o['s_off'] = _pack_conv_f8(g, w, b, o['cin'])
+                o['wfmt'], o['xscale'] = L.WFMT_FP8, float(fp8[idx])
+            else:
+                o['w_off'], o['b_off'] = _pack_conv(g, w, b, o['cin'])
     g.layer_tensor = {i: (loc[i][0], loc[i][1], ch[i]) for i in loc}
     return g
 
@@ -393,6 +440,7 @@ def _merge_siblings(g: Graph):
                         m['_w'] = torch.cat([lo['_w'], hi['_w']], 0)
                         m['_b'] = torch.cat([lo['_b'], hi['_b']], 0)
                         m['merged'] = (lo['cout'], hi['cout'])
+                        m['layers'] = lo['layers'] + hi['layers']
                         g.ops[i] = m
                         del g.ops[j]
                         break

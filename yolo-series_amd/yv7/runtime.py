@@ -8,6 +8,7 @@ and the whole network is one yv7_forward call on the current stream.
 from __future__ import annotations
 
 import ctypes
+import math
 import weakref
 
 import torch
@@ -52,7 +53,7 @@ class Plan:
         ops = []
         for o in graph.ops:
             d = dict(kind=0, src=0, src_coff=0, cin=0, dst=0, dst_coff=0, cout=0, k=1, s=1, pad=0, act=0, level=0,
-                     w_off=0, b_off=0, cout2=0, act2=0, w2_off=0, b2_off=0)
+                     w_off=0, b_off=0, cout2=0, act2=0, w2_off=0, b2_off=0, wfmt=0, xscale=0.0, s_off=0)
             d.update({k: v for k, v in o.items() if k in d})
             ops.append(L.OpDesc(**d))
         self._ops = (L.OpDesc * len(ops))(*ops)
@@ -71,12 +72,46 @@ class Plan:
         self.weight_bytes = weights.numel()
 
     @classmethod
-    def from_model(cls, model, device, dtype=torch.float32, weights=None):
+    def from_model(cls, model, device, dtype=torch.float32, weights=None, calib=None):
+        """dtype: torch.float32 / torch.float16, or 'fp8' (fp16 plan whose 1x1 convs run in e4m3, see
+        fp8_from_model; `calib` then gives its calibration frames)."""
+        if isinstance(dtype, str) and dtype == 'fp8':
+            return cls.fp8_from_model(model, device, calib=calib)
         code = L.DT_F16 if dtype == torch.float16 else L.DT_F32
         g = compile_model(model, code)
         blob = g.weight_blob() if weights is None else weights
         blob = blob.to(device)
         return cls(g, device, blob)
+
+    @classmethod
+    def fp8_from_model(cls, model, device, calib=None):
+        """BASELINE configs[4]: the fp16 plan with every 1x1 stride-1 conv (the Detect head excepted) on
+        OCP e4m3 weights (per-output-channel scales) and e4m3 activations (per-tensor power-of-two
+        scales), through the block-scaled fp8 MFMA (csrc/conv_f8.hip).
+
+        Activation scales come from calibration: the fp16 plan runs `calib` ([B,3,H,W] frames in [0,1];
+        default: 2 seeded synthetic frames at the model's native size) and each fp8 op's input amax
+        sets xscale = 2**ceil(log2(amax / 448)), so the largest calibrated value still fits e4m3."""
+        from yv7.graph import fp8_candidates
+        base = cls.from_model(model, device, torch.float16)
+        if calib is None:
+            from yv7.synthetic import synthetic_frames
+            hw = 1280 if float(model.stride.max()) >= 64 else 640
+            calib = synthetic_frames(2, hw, hw, seed=4321)
+        x = calib.to(base.device).half()
+        B, _, H, W = x.shape
+        N = base.num_rows(H, W)
+        z = torch.empty((B, N, base.no), dtype=torch.float32, device=base.device)
+        base.forward_into(x, z)
+        scales = {}
+        for i in fp8_candidates(base.graph):
+            o = base.graph.ops[i]
+            v = base.tensor_view(o['src'], B, H, W)[..., o['src_coff']:o['src_coff'] + o['cin']]
+            amax = float(v.abs().max().float())
+            scales[i] = 2.0 ** math.ceil(math.log2(amax / 448.0)) if amax > 0 else 1.0
+        g = compile_model(model, L.DT_F16, fp8=scales)
+        del base
+        return cls(g, device, g.weight_blob().to(device))
 
     def __del__(self):
         h = getattr(self, '_h', None)
@@ -116,6 +151,15 @@ class Plan:
         t = ws[off.value:off.value + n * es].view(torch.float16 if es == 2 else torch.float32)
         bd = L.BORDER   # bordered layout (include/yv7.h YV7_BORDER): return the image interior
         return t.view(dims[0], dims[1], dims[2], dims[3])[:, bd:dims[1] - bd, bd:dims[2] - bd]
+
+    def f8_scratch(self, B, H, W):
+        """uint8 view of the fp8 staging buffer (the last FP8 op's e4m3 input after a forward), or None."""
+        off, n = ctypes.c_int64(), ctypes.c_int64()
+        L.check(L.lib().yv7_f8_scratch_info(self._h, B, H, W, ctypes.byref(off), ctypes.byref(n)),
+                'yv7_f8_scratch_info')
+        if n.value == 0:
+            return None
+        return self.workspace(B, H, W)[off.value:off.value + n.value]
 
     def layer_output(self, layer_i, B, H, W):
         """NCHW fp32 copy of layer `layer_i`'s output from the last forward."""
