@@ -80,9 +80,21 @@ def test_bus_jpg_detect_fp32():
 
 @pytest.mark.gpu
 def test_bus_jpg_detect_fp16_map():
-    from oracle import metrics_ref
-    _, _, _, _, det_r = _oracle_bus()
+    """detect.py's default half() path, judged like the reference's own half() path: mAP@0.5 of the
+    detections against the oracle's fp32 ones, next to the oracle's fp16-storage emulation of the
+    reference half path on the same frame (bus.jpg lights up ~20k candidate rows of this synthetic
+    head, so the 300-detection cut falls among near-tied scores and costs both paths the same)."""
+    from oracle import metrics_ref, nms_ref, yolo_ref
+    img0, _, x, _, det_r = _oracle_bus()
+    net, fused = oracle_net('yolov7-tiny')
+    with torch.no_grad():
+        ze, _ = yolo_ref.forward(net, fused, x, half_storage=True)
+    de = nms_ref.non_max_suppression(ze, 0.25, 0.45)[0]
+    de[:, :4] = nms_ref.scale_coords(x.shape[2:], de[:, :4], img0.shape).round()
+    truth = [metrics_ref.dets_as_labels(det_r)]
+    emu, _ = metrics_ref.map_from_lists([de], truth)
     (path, det), = _detect(fp32=False)
-    m50, _ = metrics_ref.map_from_lists([det], [metrics_ref.dets_as_labels(det_r)])
-    print(f'\nbus.jpg yolov7-tiny fp16: {len(det)} dets (oracle fp32 {len(det_r)}), mAP@0.5 {m50:.4f}')
-    assert m50 >= 0.95
+    m50, _ = metrics_ref.map_from_lists([det], truth)
+    print(f'\nbus.jpg yolov7-tiny fp16: {len(det)} dets (oracle fp32 {len(det_r)}), mAP@0.5 {m50:.4f} '
+          f'(reference-half emulation {emu:.4f})')
+    assert m50 >= emu - 0.02

@@ -133,4 +133,40 @@ def test_gpu_fp8_map_parity(name):
     emu32, _ = metrics_ref.map_from_lists([d for d in nms_ref.non_max_suppression(ze, 0.25, 0.45)], gt)
     print(f'\n{name} fp8: mAP@0.5 vs fp32 oracle {m32:.4f} (oracle fp8 restatement vs fp32: {emu32:.4f}), '
           f'vs fp8 restatement {memu:.4f}; dets {[len(d) for d in pred]}')
-    assert m32 >= 0.5 and memu >= 0.5
+    # e4m3 costs this random-weight network most of its detections (the restatement loses as much as the
+    # kernels do); the GPU plan must be no worse than the restatement of its own arithmetic
+    assert m32 >= emu32 - 0.1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name', ['yolov7', 'yolov7-tiny'])
+def test_gpu_fp8_layerwise(name):
+    """Every fp8 op of a GPU forward against the restatement applied to the very fp16 input the op read
+    (so the comparison does not depend on upstream rounding): e4m3 input on the op's scale, the plan's
+    e4m3 weights and scales, fp32 accumulation, bias, activation.  Output within 2e-3 of max|y| (fp16
+    output rounding plus accumulation order)."""
+    import torch.nn.functional as F
+    B, H, W = 1, 128, 128
+    x = frames(B, H, W, seed=9)
+    plan = _gpu_fp8_plan(name, x)
+    z = torch.empty(B, plan.num_rows(H, W), plan.no, device='cuda:0')
+    plan.forward_into(x.cuda().half(), z)
+    torch.cuda.synchronize()
+    blob = plan.graph.weight_blob()
+    acts = {L.ACT_SILU: F.silu, L.ACT_LEAKY: lambda t: F.leaky_relu(t, 0.1), L.ACT_NONE: lambda t: t}
+    worst = 0.0
+    n = 0
+    for o in plan.graph.ops:
+        if o.get('wfmt', 0) != L.WFMT_FP8:
+            continue
+        xin = plan.tensor_view(o['src'], B, H, W)[..., o['src_coff']:o['src_coff'] + o['cin']].float().cpu()
+        xq = yolo_ref.fp8_e4m3(xin / o['xscale']) * o['xscale']
+        w = plan_interp._weights_f8(blob, o['w_off'], o['cout'], o['cin'], o['s_off']).reshape(o['cout'], -1)
+        b = plan_interp._bias(blob, o['b_off'], o['cout'])
+        want = acts[o['act']](xq @ w.t() + b)
+        got = plan.tensor_view(o['dst'], B, H, W)[..., o['dst_coff']:o['dst_coff'] + o['cout']].float().cpu()
+        err = ((got - want).abs().max() / want.abs().max().clamp(min=1e-3)).item()
+        worst = max(worst, err)
+        n += 1
+    print(f'\n{name}: {n} fp8 ops, worst max-norm rel err {worst:.3g}')
+    assert n > 10 and worst < 2e-3
