@@ -86,6 +86,9 @@ typedef struct {
   int32_t wfmt;                /* CONV: yv7_wfmt */
   float xscale;                /* CONV, wfmt FP8: per-tensor input scale (a power of two) */
   int64_t s_off;               /* CONV, wfmt FP8: byte offset of fp32 weight scales [cout] */
+  int32_t pool;                /* CONV (fp16 plans, 1x1): 2 = the input is first max-pooled 2x2 / stride 2 (an MP
+                                  layer, common.py:30-36, folded into the conv's operand loads); then s = 2 */
+  int32_t reserved;
 } yv7_op_desc;
 
 typedef struct {

@@ -26,6 +26,7 @@ __global__ void fill_rand(_Float16* p, size_t n, uint32_t seed, float scale) {
 int main(int argc, char** argv) {
   std::vector<Shape> shapes = {
     {"3x3 64->64 @320", 32, 320, 320, 64, 64, 3, 1},
+    {"3x3s2 64->128 @320", 32, 320, 320, 64, 128, 3, 2},
     {"3x3 64->64 @160", 32, 160, 160, 64, 64, 3, 1},
     {"3x3 64->64 @80", 32, 80, 80, 64, 64, 3, 1},
     {"3x3 128->64 @80", 32, 80, 80, 128, 64, 3, 1},

@@ -4,6 +4,7 @@
 //        -L yolo-series_amd/yv7 -lyv7 -Wl,-rpath,'$ORIGIN/../yolo-series_amd/yv7' -o scripts/stembench
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include "yv7_kernels.h"
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("HIP %s line %d\n", hipGetErrorString(e), __LINE__); return 1; } } while (0)
@@ -13,7 +14,7 @@ __global__ void fill(_Float16* p, size_t n, float scale) {
     p[i] = (_Float16)(((h & 0xffff) / 65536.0f) * scale);
   }
 }
-int main() {
+int main(int argc, char** argv) {
   const int B = 32, H = 640, W = 640;
   _Float16 *x, *y, *wa, *wb; float *ba, *bb;
   const size_t ny = yv7::bordered_pixels(B, H / 2, W / 2) * 64;
@@ -26,6 +27,7 @@ int main() {
   CK(hipMemset(ba, 0, 32 * 4)); CK(hipMemset(bb, 0, 64 * 4)); CK(hipMemset(y, 0, ny * 2));
   yv7::StemParams p; memset(&p, 0, sizeof(p));
   p.x = x; p.y = y; p.wa = wa; p.ba = ba; p.wb = wb; p.bb = bb;
+  p.variant = argc > 1 ? atoi(argv[1]) : 0;
   p.B = B; p.H = H; p.W = W; p.yc = 64; p.yoff = 0; p.kpad_a = 64; p.kpad_b = 320; p.act_a = 1; p.act_b = 1; p.sa = 1;
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (int i = 0; i < 3; ++i) CK(yv7::launch_stem(p, 1, 0));
@@ -35,6 +37,6 @@ int main() {
   CK(hipEventRecord(e1, 0)); CK(hipEventSynchronize(e1));
   float ms; CK(hipEventElapsedTime(&ms, e0, e1)); ms /= 20;
   const double fl = 2.0 * B * H * W * 32 * 27 + 2.0 * B * (H / 2) * (W / 2) * 64 * 288;
-  printf("stem bs32 640: %.1f us  %.0f TF/s\n", ms * 1e3, fl / ms / 1e9);
+  printf("stem bs32 640 variant %d: %.1f us  %.0f TF/s\n", p.variant, ms * 1e3, fl / ms / 1e9);
   return 0;
 }

@@ -65,13 +65,16 @@ def run(g, x: torch.Tensor, return_tensors=False):
             T[o['dst']][:, o['dst_coff']:o['dst_coff'] + o['cout2']] = y
         elif kind == L.OP_CONV:
             src = T[o['src']][:, o['src_coff']:o['src_coff'] + o['cin']]
+            if o.get('pool', 0) == 2:   # MP folded into the conv (yv7.graph._fold_pools)
+                src = F.max_pool2d(src, 2, 2)
             if o.get('wfmt', 0) == L.WFMT_FP8:   # e4m3 input on the op's scale, e4m3 weights
                 xs = o['xscale']
                 src = (src / xs).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).float() * xs
                 w = _weights_f8(blob, o['w_off'], o['cout'], o['cin'], o['s_off'])
             else:
                 w = _weights(blob, g.dtype, o['w_off'], o['cout'], o['k'], o['cin'])
-            y = _act(F.conv2d(src, w, _bias(blob, o['b_off'], o['cout']), o['s'], o['pad']), o['act'])
+            y = _act(F.conv2d(src, w, _bias(blob, o['b_off'], o['cout']), 1 if o.get('pool', 0) else o['s'],
+                              o['pad']), o['act'])
             T[o['dst']][:, o['dst_coff']:o['dst_coff'] + o['cout']] = y
         elif kind == L.OP_MAXPOOL:
             src = T[o['src']][:, o['src_coff']:o['src_coff'] + o['cout']]

@@ -47,7 +47,7 @@ def test_fp8_graph_packing():
     x = frames(1, 64, 64, seed=2)
     g16, g8 = _calibrated_fp8_graph(m, x)
     f8 = [o for o in g8.ops if o.get('wfmt', 0) == L.WFMT_FP8]
-    assert len(f8) == len(fp8_candidates(g16)) > 30
+    assert len(f8) == len(fp8_candidates(g16)) > 25
     assert all(o['kind'] == L.OP_CONV and o['k'] == 1 for o in f8)
     assert not any(o.get('wfmt', 0) for o in g8.ops if o['kind'] == L.OP_DETECT)
     for o in f8:
@@ -68,21 +68,34 @@ def test_fp8_graph_packing():
 
 @pytest.mark.parametrize('name', ['yolov7', 'yolov7-tiny'])
 def test_fp8_plan_semantics_vs_oracle_emulation(name):
-    """The compiled fp8 plan run op by op on the CPU equals the oracle's fp8 restatement (same
-    quantization points and scales) up to fp32 summation order and fp16 weight storage."""
+    """Every fp8 op of the compiled plan, run by the CPU interpreter, against the oracle's restatement
+    (oracle.yolo_ref.fp8_fused: its own per-channel e4m3 quantization of the fused fp32 weights, e4m3
+    input on the op's scale) applied to the same input tensor.  Per op, because e4m3 rounding makes the
+    whole random-weight network chaotic: a 1e-6 upstream difference flips roundings that compound over
+    40 quantized layers (end-to-end z differs by several %; mAP is the end-to-end criterion)."""
+    import torch.nn.functional as F
     m = fresh_model(name)
     x = frames(1, 128, 128, seed=3)
     _, g8 = _calibrated_fp8_graph(m, x)
     net, fused = oracle_net(name)
-    emu = yolo_ref.half_weights(yolo_ref.fp8_fused(fused, _entries(g8)))
+    emu = yolo_ref.fp8_fused(fused, _entries(g8))
     with torch.no_grad():
-        got = plan_interp.run(g8, x)
-        want = yolo_ref.forward(net, emu, x)[0]
-    rel = ((got - want).pow(2).mean().sqrt() / want.pow(2).mean().sqrt()).item()
-    assert rel < 2e-3, rel
-    gt = [metrics_ref.dets_as_labels(d) for d in nms_ref.non_max_suppression(want, 0.25, 0.45)]
-    m50, _ = metrics_ref.map_from_lists(nms_ref.non_max_suppression(got, 0.25, 0.45), gt)
-    assert m50 >= 0.98, m50
+        _, T = plan_interp.run(g8, x, return_tensors=True)
+    acts = {L.ACT_SILU: F.silu, L.ACT_LEAKY: lambda t: F.leaky_relu(t, 0.1), L.ACT_NONE: lambda t: t}
+    n = 0
+    for o in g8.ops:
+        if o.get('wfmt', 0) != L.WFMT_FP8:
+            continue
+        parts = [emu[l] if sub is None else emu[l][sub] for l, sub in o['layers']]
+        w = torch.cat([p[0] for p in parts], 0)
+        b = torch.cat([p[1] for p in parts], 0)
+        assert all(p[2] == o['xscale'] for p in parts)
+        xin = T[o['src']][:, o['src_coff']:o['src_coff'] + o['cin']]
+        want = acts[o['act']](F.conv2d(yolo_ref.fp8_e4m3(xin / o['xscale']) * o['xscale'], w, b))
+        got = T[o['dst']][:, o['dst_coff']:o['dst_coff'] + o['cout']]
+        torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5 * float(want.abs().max()))
+        n += 1
+    assert n > 20
 
 
 # ------------------------------------------------------------------------------------------ GPU

@@ -267,6 +267,7 @@ bool det_writes_rowbest(int dtype) { return dtype == 1 && !use_v1(); }
 hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t st) {
   // fp16: the tuned kernel of conv_f16.hip (YV7_CONV_V1=1 selects this file's generic kernel, for A/B)
   const bool v1 = use_v1();
+  if (p.pool) return dtype == 1 ? launch_conv_f16(p, detect, st) : hipErrorInvalidValue;   // MP-folded 1x1
   // cout <= 32 (the stem of every model, tiny's narrow layers): this kernel's BK=32 steps waste less
   // of the short, padded K than the 64-deep steps of conv_f16 (measured: scripts/convbench.hip)
   if (dtype == 1)

@@ -370,7 +370,16 @@ __device__ __forceinline__ void det_tail(const ConvParams& p, unsigned char* sme
   }
 }
 
-template <int BM, int BN, int WM, bool ONE, bool DET, int PF = 1>
+// 2x2 max of four 16-byte fp16 vectors (MP folded into a 1x1 conv's operand loads)
+__device__ __forceinline__ u4 hmax4(u4 a, u4 b, u4 c, u4 d) {
+  const h8 m = __builtin_elementwise_max(__builtin_elementwise_max(__builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b)),
+                                         __builtin_elementwise_max(__builtin_bit_cast(h8, c), __builtin_bit_cast(h8, d)));
+  return __builtin_bit_cast(u4, m);
+}
+
+// POOL: 1x1 conv over the 2x2 / stride-2 max of the input (ConvParams::pool; k = 1, s = 2, pad = 0): each A
+// row's origin is the window's top-left pixel, the other three are fixed byte offsets.
+template <int BM, int BN, int WM, bool ONE, bool DET, int PF = 1, bool POOL = false>
 __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   constexpr int WN = 4 / WM;
   constexpr int WTM = BM / WM, WTN = BN / WN;
@@ -416,9 +425,18 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)(((n0 + r0 + 32 * j) * p.kpad + c * 8) * 2);
 
   const int nk = p.kpad / BKE;
+  const uint32_t pdx = (uint32_t)p.xc * 2, pdy = (uint32_t)(p.W + 2 * BORDER) * p.xc * 2;   // POOL window steps
   auto gload = [&](int kt, u4 (&ra)[RA], u4 (&rb)[RB]) {
     aw.step(p, kt, [&](int j, uint32_t vo, uint32_t so) {
-      ra[j] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, so, 0));
+      if constexpr (POOL) {
+        const u4 a = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, so, 0));
+        const u4 b = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo + pdx, so, 0));
+        const u4 c2 = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo + pdy, so, 0));
+        const u4 d = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo + pdy + pdx, so, 0));
+        ra[j] = hmax4(a, b, c2, d);
+      } else {
+        ra[j] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, vo, so, 0));
+      }
     });
 #pragma unroll
     for (int j = 0; j < RB; ++j)
@@ -1037,10 +1055,10 @@ hipError_t launch_ring2(const ConvParams& p, bool one, hipStream_t st) {
   return one ? launch_ring<BM, BN, WM, WN, STAGES, true>(p, st) : launch_ring<BM, BN, WM, WN, STAGES, false>(p, st);
 }
 
-template <int BM, int BN, int WM, bool ONE, bool DET, int PF = 1>
+template <int BM, int BN, int WM, bool ONE, bool DET, int PF = 1, bool POOL = false>
 hipError_t launch_t(const ConvParams& p, hipStream_t st) {
   const int nM = (p.M + BM - 1) / BM, nN = (p.cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, ONE, DET, PF>), dim3(nM * nN), dim3(NT), 0, st, p);
+  hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, ONE, DET, PF, POOL>), dim3(nM * nN), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 
@@ -1143,6 +1161,11 @@ int conv_splitk_tiles(const ConvParams& p) {
 hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   const bool one = p.k == 1 && p.s == 1 && p.pad == 0;
   const int variant = p.variant ? p.variant : env_variant();
+  if (p.pool) {   // MP folded into a 1x1 conv: register-staged tile kernel (the max needs the operands in VGPRs)
+    if (p.pool != 2 || p.k != 1 || p.s != 2 || p.pad != 0 || det || p.cin % 64) return hipErrorInvalidValue;
+    if (p.cout <= 64) return launch_t<128, 64, 2, false, false, 1, true>(p, st);
+    return launch_t<128, 128, 2, false, false, 1, true>(p, st);
+  }
   if (!det && variant == 0 && p.cout > 32 && p.cout <= 1024 && p.cout % 8 == 0) {
     // Persistent ring (scripts/convbench.hip, bs 32, same box, us): short-K 1x1 layers and the
     // 128-channel / low-resolution 512-channel 3x3 layers, whose per-tile fill + epilogue the

@@ -121,6 +121,7 @@ yv7::ConvParams conv_params(const yv7_plan* p, const yv7_op_desc& o, int B, int 
   c.s = o.s;
   c.pad = o.pad;
   c.act = o.act;
+  c.pool = o.kind == YV7_OP_CONV ? o.pool : 0;
   c.kpad = kpad_of(o);
   c.K = o.k * o.k * o.cin;
   c.M = B * c.Ho * c.Wo;
@@ -190,6 +191,10 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
     if (o.kind == YV7_OP_CONV || o.kind == YV7_OP_DETECT) {
       if (o.cin % vec || (o.kind == YV7_OP_CONV && o.cout % vec))
         return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) + " channels not a multiple of the vector");
+      if (o.kind == YV7_OP_CONV && o.pool != 0 &&
+          (o.pool != 2 || d->dtype != YV7_DT_F16 || o.k != 1 || o.s != 2 || o.pad != 0 || o.wfmt != YV7_WFMT_PLAN))
+        return fail(YV7_E_ARG, "yv7_plan_create: op " + std::to_string(i) +
+                                   " bad pooled conv (fp16 plans, pool 2 with k 1, s 2, pad 0)");
       if (o.kind == YV7_OP_CONV && o.wfmt != YV7_WFMT_PLAN) {
         if (o.wfmt != YV7_WFMT_FP8 || d->dtype != YV7_DT_F16 || o.k != 1 || o.s != 1 || o.pad != 0 ||
             o.cout > 1024 || !(o.xscale > 0.0f) || o.xscale > 1e30f || o.s_off < 0 ||
@@ -481,6 +486,7 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
         if ((H >> to.shift) != H / o.s / 2 || (W >> to.shift) != W / o.s / 2)
           return fail(YV7_E_SHAPE, "yv7_forward: stem output shape mismatch");
         yv7::StemParams sp;
+        sp.variant = 0;
         sp.x = x;
         sp.y = wsb + off[o.dst];
         sp.wa = wb + o.w_off;

@@ -69,7 +69,7 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
     const int iy = iy0 + py, ix = ix0 + px;
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     h4 v = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
-    if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W) {
+    if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2) {
       const size_t o = (size_t)iy * p.W + ix;
       v[0] = (_Float16)(float)xb[o];
       v[1] = (_Float16)(float)xb[o + (size_t)p.H * p.W];
@@ -158,7 +158,8 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         float v;
-        if constexpr (ACT_A == 1) v = acc[e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[e]));
+        if (p.variant == 1) v = acc[e];
+        else if constexpr (ACT_A == 1) v = acc[e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[e]));
         else v = act_t<ACT_A>(acc[e]);
         o[e] = inside ? (_Float16)v : (_Float16)0.f;
       }
@@ -179,6 +180,7 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   }
 #pragma unroll
   for (int tap = 0; tap < 9; ++tap) {
+    if (p.variant == 3) break;   // microbenchmark hook: no conv B
     const int r = tap / 3, s = tap - r * 3;
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
@@ -220,7 +222,7 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
     const int mb = c / CPR, ch = c - mb * CPR;
     const int ty = mb / TBX, tx = mb - ty * TBX;
     const int oy = oy0 + ty, ox = ox0 + tx;
-    if (oy < HB && ox < WB)
+    if (oy < HB && ox < WB && p.variant != 4)
       *reinterpret_cast<u4*>(y + pix_index(b, oy, ox, HB, WB) * p.yc + p.yoff + ch * 8) =
           *reinterpret_cast<const u4*>(smem + mb * CPITCH + ch * 16);
   }

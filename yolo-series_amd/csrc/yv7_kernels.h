@@ -78,6 +78,7 @@ struct ConvParams {
   size_t part_bytes;
   int cnt_n;
   int ksplit;
+  int pool;           // 2: 1x1 conv over the 2x2 / stride-2 max of the input (MP folded in; k = 1, s = 2)
 };
 
 // Split-K scratch the fp16 dispatch needs for one conv (0 when it does not split).
@@ -109,6 +110,7 @@ struct StemParams {
   const void* wb;       // conv-B weights [64][kpad_b] (k = tap*32 + ci)
   const float* bb;
   int B, H, W, yc, yoff, kpad_a, kpad_b, act_a, act_b, sa;
+  int variant;          // 0; >0: microbenchmark hooks (scripts/stembench.hip)
 };
 
 // Host launchers (defined in the .hip files, called from the runtime).

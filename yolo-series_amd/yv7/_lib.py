@@ -34,7 +34,8 @@ class OpDesc(ctypes.Structure):
                 ('w_off', ctypes.c_int64), ('b_off', ctypes.c_int64),
                 ('cout2', ctypes.c_int32), ('act2', ctypes.c_int32),
                 ('w2_off', ctypes.c_int64), ('b2_off', ctypes.c_int64),
-                ('wfmt', ctypes.c_int32), ('xscale', ctypes.c_float), ('s_off', ctypes.c_int64)]
+                ('wfmt', ctypes.c_int32), ('xscale', ctypes.c_float), ('s_off', ctypes.c_int64),
+                ('pool', ctypes.c_int32), ('reserved', ctypes.c_int32)]
 
 
 class NetDesc(ctypes.Structure):

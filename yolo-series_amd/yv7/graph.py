@@ -345,7 +345,8 @@ def compile_model(model, dtype: int, fp8=None) -> Graph:
             k = p.kernel_size if isinstance(p.kernel_size, int) else p.kernel_size[0]
             st = p.stride if isinstance(p.stride, int) else p.stride[0]
             pd = p.padding if isinstance(p.padding, int) else p.padding[0]
-            g.ops.append(dict(kind=L.OP_MAXPOOL, src=ts, src_coff=so, dst=td, dst_coff=do, cout=cs, k=k, s=st, pad=pd))
+            g.ops.append(dict(kind=L.OP_MAXPOOL, src=ts, src_coff=so, dst=td, dst_coff=do, cout=cs, k=k, s=st, pad=pd,
+                              layer=i))
         elif isinstance(m, nn.Upsample):
             (ts, so, cs), (td, do) = src_of(i, m.f), out_of(i)
             g.ops.append(dict(kind=L.OP_UPSAMPLE, src=ts, src_coff=so, dst=td, dst_coff=do, cout=cs))
@@ -368,6 +369,7 @@ def compile_model(model, dtype: int, fp8=None) -> Graph:
                 w_off, b_off = _pack_conv(g, w, b, _rup(cs, V))
                 g.ops.append(dict(kind=L.OP_DETECT, src=ts, src_coff=so, cin=_rup(cs, V), dst=-1, cout=w.shape[0],
                                   k=1, s=1, pad=0, level=lvl, w_off=w_off, b_off=b_off))
+    folded = _fold_pools(g) if dtype == L.DT_F16 and os.environ.get('YV7_NO_POOLFOLD') != '1' else []
     if os.environ.get('YV7_NO_MERGE') != '1':
         _merge_siblings(g)
     fp8 = fp8 or {}
@@ -381,8 +383,37 @@ def compile_model(model, dtype: int, fp8=None) -> Graph:
                 o['wfmt'], o['xscale'] = L.WFMT_FP8, float(fp8[idx])
             else:
                 o['w_off'], o['b_off'] = _pack_conv(g, w, b, o['cin'])
-    g.layer_tensor = {i: (loc[i][0], loc[i][1], ch[i]) for i in loc}
+    g.layer_tensor = {i: (loc[i][0], loc[i][1], ch[i]) for i in loc if i not in folded}
     return g
+
+
+def _fold_pools(g: Graph):
+    """MP (2x2 / stride-2 max, models/common.py:30-36) whose output only feeds one 1x1 conv (every MP of the
+    yolov7 family: `[-1, 1, MP, []], [-1, 1, Conv, [c, 1, 1]]`) -> that conv reads the MP's input with
+    pool = 2, s = 2: the max is taken in the conv's operand loads and the pooled tensor never reaches
+    HBM.  Returns the folded MP layers (their outputs no longer exist as tensors)."""
+    folded = []
+    i = 0
+    while i < len(g.ops):
+        mp = g.ops[i]
+        if not (mp['kind'] == L.OP_MAXPOOL and mp['k'] == 2 and mp['s'] == 2 and mp['pad'] == 0):
+            i += 1
+            continue
+        t = mp['dst']
+        readers = [j for j, o in enumerate(g.ops) if j != i and o.get('src', -1) == t]
+        writers = [j for j, o in enumerate(g.ops) if j != i and _writes(o) and _writes(o)[0] == t]
+        ok = len(readers) == 1 and not writers and readers[0] > i
+        if ok:
+            c = g.ops[readers[0]]
+            ok = (c['kind'] == L.OP_CONV and '_w' in c and c['k'] == 1 and c['s'] == 1 and c['pad'] == 0 and
+                  c['src_coff'] == mp['dst_coff'] and c['cin'] == mp['cout'] and c['cin'] % 64 == 0)
+        if not ok:
+            i += 1
+            continue
+        c.update(src=mp['src'], src_coff=mp['src_coff'], s=2, pool=2)
+        folded.append(mp.get('layer'))
+        del g.ops[i]
+    return folded
 
 
 def _writes(o):

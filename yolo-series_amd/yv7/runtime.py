@@ -53,7 +53,7 @@ class Plan:
         ops = []
         for o in graph.ops:
             d = dict(kind=0, src=0, src_coff=0, cin=0, dst=0, dst_coff=0, cout=0, k=1, s=1, pad=0, act=0, level=0,
-                     w_off=0, b_off=0, cout2=0, act2=0, w2_off=0, b2_off=0, wfmt=0, xscale=0.0, s_off=0)
+                     w_off=0, b_off=0, cout2=0, act2=0, w2_off=0, b2_off=0, wfmt=0, xscale=0.0, s_off=0, pool=0)
             d.update({k: v for k, v in o.items() if k in d})
             ops.append(L.OpDesc(**d))
         self._ops = (L.OpDesc * len(ops))(*ops)
@@ -210,7 +210,10 @@ class Plan:
                 flops = 2.0 * B * Ho * Wo * cout * k * k * cin
                 wbytes = cout * k * k * cin * es + cout * 4
                 obytes = B * Ho * Wo * cout * (es if kind == L.OP_CONV else (8 if with_raw else 4))
-                out.append((kind, flops, B * Hi * Wi * cin * es + obytes + wbytes))
+                # an MP folded into the conv (pool 2): the reference-boundary bytes of both layers, i.e.
+                # also the pooled tensor's write and re-read
+                mp = 2 * B * Ho * Wo * cin * es if o.get('pool', 0) == 2 else 0
+                out.append((kind, flops, B * Hi * Wi * cin * es + obytes + wbytes + mp))
             elif kind == L.OP_MAXPOOL:
                 c = o['cout']
                 out.append((kind, 0.0, B * Hi * Wi * c * es + B * Ho * Wo * c * es))
