@@ -1163,8 +1163,12 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   const int variant = p.variant ? p.variant : env_variant();
   if (p.pool) {   // MP folded into a 1x1 conv: register-staged tile kernel (the max needs the operands in VGPRs)
     if (p.pool != 2 || p.k != 1 || p.s != 2 || p.pad != 0 || det || p.cin % 64) return hipErrorInvalidValue;
+    // in-network A/B over the five yolov7 MP+1x1 pairs (us, 128x128 / 64x128): 256->128 @160 111 / 104,
+    // 512->256 @80 71 / 68, 256->256 @40 16.9 / 15.1 (1024->512 @40 folds no more: 52 vs 46.5 unfused)
+    static const int pcfg = [] { const char* e = getenv("YV7_POOL_CFG"); return e ? atoi(e) : 0; }();
     if (p.cout <= 64) return launch_t<128, 64, 2, false, false, 1, true>(p, st);
-    return launch_t<128, 128, 2, false, false, 1, true>(p, st);
+    if (pcfg == 1) return launch_t<128, 128, 2, false, false, 1, true>(p, st);
+    return launch_t<64, 128, 1, false, false, 1, true>(p, st);
   }
   if (!det && variant == 0 && p.cout > 32 && p.cout <= 1024 && p.cout % 8 == 0) {
     // Persistent ring (scripts/convbench.hip, bs 32, same box, us): short-K 1x1 layers and the

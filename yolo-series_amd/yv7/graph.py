@@ -388,8 +388,8 @@ def compile_model(model, dtype: int, fp8=None) -> Graph:
 
 
 def _fold_pools(g: Graph):
-    """MP (2x2 / stride-2 max, models/common.py:30-36) whose output only feeds one 1x1 conv (every MP of the
-    yolov7 family: `[-1, 1, MP, []], [-1, 1, Conv, [c, 1, 1]]`) -> that conv reads the MP's input with
+    """MP (2x2 / stride-2 max, models/common.py:30-36) whose output only feeds one 1x1 conv of <= 512 input
+    channels (yolov7: `[-1, 1, MP, []], [-1, 1, Conv, [c, 1, 1]]`) -> that conv reads the MP's input with
     pool = 2, s = 2: the max is taken in the conv's operand loads and the pooled tensor never reaches
     HBM.  Returns the folded MP layers (their outputs no longer exist as tensors)."""
     folded = []
@@ -406,7 +406,8 @@ def _fold_pools(g: Graph):
         if ok:
             c = g.ops[readers[0]]
             ok = (c['kind'] == L.OP_CONV and '_w' in c and c['k'] == 1 and c['s'] == 1 and c['pad'] == 0 and
-                  c['src_coff'] == mp['dst_coff'] and c['cin'] == mp['cout'] and c['cin'] % 64 == 0)
+                  c['src_coff'] == mp['dst_coff'] and c['cin'] == mp['cout'] and c['cin'] % 64 == 0 and
+                  c['cin'] <= 512)   # deep-K (1024) pairs run faster unfused (csrc/conv_f16.hip, pool dispatch)
         if not ok:
             i += 1
             continue
