@@ -52,6 +52,8 @@ def parse():
     ap.add_argument('--split', type=int, default=1, help='run the batch as this many concurrent sub-batches, '
                     'each on its own HIP stream and workspace (fills the low-resolution layers\' tails and the '
                     'kernel-boundary gaps of one stream with the other\'s work)')
+    ap.add_argument('--no-pipeline', action='store_true', help='run each batch\'s NMS (+ detection all-gather) '
+                    'on the forward\'s stream instead of overlapping it with the next batch\'s forward')
     ap.add_argument('--graph', action='store_true', help='replay the step as a HIP graph (measured: same speed '
                     'as eager launches on MI355X, the inter-kernel gaps are dependency drains, not launch cost)')
     return ap.parse_args()
@@ -140,11 +142,22 @@ def main():
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
     x = (torch.randint(0, 256, (B, 3, H, W), generator=g, device=dev, dtype=torch.uint8).to(dt) / 255.0)
     N = plan.num_rows(H, W)
-    z = torch.empty((B, N, plan.no), dtype=torch.float32, device=dev)
-    det = torch.empty((B, 300, 6), dtype=torch.float32, device=dev)
-    src = torch.empty((B, 300), dtype=torch.int64, device=dev)
-    cnt = torch.empty((B,), dtype=torch.int32, device=dev)
-    rowbest = torch.empty((B, N, 4), dtype=torch.float32, device=dev)   # yv7_row_best records
+    # Serving pipeline: batch k's NMS (and on multi-GPU its detection all-gather) runs on a second HIP
+    # stream while batch k+1's forward runs on the first, so z / row records / detections are double
+    # buffered and HIP events order each buffer's reuse.  --no-pipeline (and --graph) run the whole
+    # step on one stream.
+    pipeline = not (a.no_pipeline or a.graph)
+    nbuf = 2 if pipeline else 1
+    zs = [torch.empty((B, N, plan.no), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+    dets = [torch.empty((B, 300, 6), dtype=torch.float32, device=dev) for _ in range(nbuf)]
+    srcs = [torch.empty((B, 300), dtype=torch.int64, device=dev) for _ in range(nbuf)]
+    cnts = [torch.empty((B,), dtype=torch.int32, device=dev) for _ in range(nbuf)]
+    rowbests = [torch.empty((B, N, 4), dtype=torch.float32, device=dev) for _ in range(nbuf)]  # yv7_row_best
+    z, det, src, cnt, rowbest = zs[0], dets[0], srcs[0], cnts[0], rowbests[0]
+    nms_stream = torch.cuda.Stream(dev) if pipeline else None
+    fwd_done = [torch.cuda.Event() for _ in range(nbuf)]
+    nms_done = [torch.cuda.Event() for _ in range(nbuf)]
+    nstep = [0]
 
     nsplit = max(1, a.split)
     if B % nsplit:
@@ -152,7 +165,7 @@ def main():
     sub = B // nsplit
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nsplit - 1)]
 
-    def forward():
+    def forward(z, rowbest):
         if nsplit == 1:
             plan.forward_into(x, z, rowbest=rowbest)
             return
@@ -165,11 +178,27 @@ def main():
         for s_ in streams[1:]:
             main.wait_stream(s_)
 
-    def step():
-        forward()
-        nms_batched(z, 0.25, 0.45, out=(det, src, cnt), rowbest=rowbest)
+    def post(k):
+        nms_batched(zs[k], 0.25, 0.45, out=(dets[k], srcs[k], cnts[k]), rowbest=rowbests[k])
         if distributed:
-            ydist.gather_detections(det, src, cnt)
+            ydist.gather_detections(dets[k], srcs[k], cnts[k])
+
+    def step():
+        k = nstep[0] % nbuf
+        nstep[0] += 1
+        if not pipeline:
+            forward(zs[k], rowbests[k])
+            post(k)
+            return
+        main = torch.cuda.current_stream(dev)
+        if nstep[0] > nbuf:
+            main.wait_event(nms_done[k])      # the NMS that read buffer k two batches ago has finished
+        forward(zs[k], rowbests[k])
+        fwd_done[k].record(main)
+        nms_stream.wait_event(fwd_done[k])
+        with torch.cuda.stream(nms_stream):
+            post(k)
+        nms_done[k].record(nms_stream)
 
     for _ in range(a.warmup):
         step()
@@ -254,7 +283,7 @@ def main():
             'vs_baseline': None,
             'dtype': a.dtype,
             'data': 'synthetic',
-            'config': {'workload': f'{a.model} P5 {H}x{W} bs={B}/GPU {a.dtype}: libyv7 forward + GPU NMS '
+            'config': {'workload': f'{a.model} {"P6" if plan.nl == 4 else "P5"} {H}x{W} bs={B}/GPU {a.dtype}: libyv7 forward + GPU NMS '
                                    f'(conf 0.25, iou 0.45, max_det 300)'
                                    + (' + RCCL all-gather of detections' if distributed else ''),
                        'global_batch': world * B, 'img': H, 'parallelism': f'dp{world}',
@@ -270,7 +299,7 @@ def main():
                          'mfma_frac': round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4)},
             'detail': {'forward_ms_events': round(fwd_ms, 3), 'conv_ms_events': round(conv_ms, 3),
                        'mean_dets_per_image': round(count_mean, 1), 'rows_per_image': N,
-                       'profiled_forwards': nf, 'hip_graph': graph is not None, 'sub_batches': nsplit},
+                       'profiled_forwards': nf, 'nms_overlapped_with_next_forward': pipeline, 'hip_graph': graph is not None, 'sub_batches': nsplit},
         }
         if not a.no_cpu_baseline and world == 1:
             res['cpu_baseline'] = cpu_baseline(a.model, a.img, a.cpu_seconds, plan=plan, dev=dev)

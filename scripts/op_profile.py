@@ -11,9 +11,9 @@ ap = argparse.ArgumentParser(); ap.add_argument('--model', default='yolov7'); ap
 ap.add_argument('--img', type=int, default=640); ap.add_argument('--dtype', default='f16'); ap.add_argument('--iters', type=int, default=10)
 ap.add_argument('--csv', default=''); ap.add_argument('--top', type=int, default=40)
 a = ap.parse_args()
-dt = torch.float16 if a.dtype == 'f16' else torch.float32
+dt = torch.float32 if a.dtype == 'f32' else torch.float16
 m = Model(a.model); synthetic_state_dict(m, seed=0); m = m.float().fuse().eval()
-plan = Plan.from_model(m, 'cuda:0', dt)
+plan = Plan.from_model(m, 'cuda:0', 'fp8' if a.dtype == 'fp8' else dt)
 B, H = a.b, a.img
 x = torch.rand(B, 3, H, H, device='cuda:0').to(dt)
 z = torch.empty(B, plan.num_rows(H, H), plan.no, device='cuda:0')

@@ -35,7 +35,7 @@ def _calibrated_fp8_graph(m, x):
     g16 = compile_model(m, L.DT_F16)
     _, T = plan_interp.run(g16, x, return_tensors=True)
     scales = {}
-    for i in fp8_candidates(g16):
+    for i in fp8_candidates(g16, 0):   # every eligible 1x1 (the product plan marks the wide ones)
         o = g16.ops[i]
         amax = float(T[o['src']][:, o['src_coff']:o['src_coff'] + o['cin']].abs().max())
         scales[i] = 2.0 ** math.ceil(math.log2(amax / 448.0)) if amax > 0 else 1.0
@@ -47,7 +47,7 @@ def test_fp8_graph_packing():
     x = frames(1, 64, 64, seed=2)
     g16, g8 = _calibrated_fp8_graph(m, x)
     f8 = [o for o in g8.ops if o.get('wfmt', 0) == L.WFMT_FP8]
-    assert len(f8) == len(fp8_candidates(g16)) > 25
+    assert len(f8) == len(fp8_candidates(g16, 0)) > 25 and len(fp8_candidates(g16)) > 10
     assert all(o['kind'] == L.OP_CONV and o['k'] == 1 for o in f8)
     assert not any(o.get('wfmt', 0) for o in g8.ops if o['kind'] == L.OP_DETECT)
     for o in f8:
@@ -99,10 +99,11 @@ def test_fp8_plan_semantics_vs_oracle_emulation(name):
 
 
 # ------------------------------------------------------------------------------------------ GPU
-def _gpu_fp8_plan(name, calib):
+def _gpu_fp8_plan(name, calib, min_cout=None):
+    """min_cout=0: every eligible 1x1 conv in fp8 (kernel coverage); None: the product plan's choice."""
     from yv7.runtime import Plan
     m = fresh_model(name).cuda().half()
-    return Plan.fp8_from_model(m, 'cuda:0', calib=calib)
+    return Plan.fp8_from_model(m, 'cuda:0', calib=calib, min_cout=min_cout)
 
 
 @pytest.mark.gpu
@@ -111,7 +112,7 @@ def test_gpu_fp8_quantizer_bit_exact():
     torch.float8_e4m3fn's bytes for the fp16 input it read (checked on the last fp8 op of a forward)."""
     B, H, W = 2, 128, 160
     x = frames(B, H, W, seed=5)
-    plan = _gpu_fp8_plan('yolov7', x)
+    plan = _gpu_fp8_plan('yolov7', x, 0)
     z = torch.empty(B, plan.num_rows(H, W), plan.no, device='cuda:0')
     plan.forward_into(x.cuda().half(), z)
     torch.cuda.synchronize()
@@ -161,7 +162,7 @@ def test_gpu_fp8_layerwise(name):
     import torch.nn.functional as F
     B, H, W = 1, 128, 128
     x = frames(B, H, W, seed=9)
-    plan = _gpu_fp8_plan(name, x)
+    plan = _gpu_fp8_plan(name, x, 0)
     z = torch.empty(B, plan.num_rows(H, W), plan.no, device='cuda:0')
     plan.forward_into(x.cuda().half(), z)
     torch.cuda.synchronize()

@@ -131,9 +131,17 @@ def fp8_eligible(g: Graph, o: dict) -> bool:
             and o['cout'] <= 1024)
 
 
-def fp8_candidates(g: Graph):
-    """Op indices of `g` that compile_model(..., fp8={index: xscale}) can mark FP8."""
-    return [i for i, o in enumerate(g.ops) if fp8_eligible(g, o)]
+# fp8 pays only on wide layers: measured per op on MI355X (bs32 640 yolov7, scripts/op_profile.py
+# --dtype fp8 vs f16), cout >= 512 gains 1-41 us per layer (1024->1024 @40: 156 -> 114 us) while every
+# cout <= 256 layer loses 3-82 us — their time is the SiLU epilogue and the extra quantize pass, not
+# the MFMA, so the 2x fp8 MFMA rate cannot win it back.
+FP8_MIN_COUT = 512
+
+
+def fp8_candidates(g: Graph, min_cout: int = FP8_MIN_COUT):
+    """Op indices of `g` that compile_model(..., fp8={index: xscale}) marks FP8 in an fp8 plan: the
+    fp8-eligible ops with at least `min_cout` output channels (min_cout=0: every eligible op)."""
+    return [i for i, o in enumerate(g.ops) if fp8_eligible(g, o) and o['cout'] >= min_cout]
 
 
 def _live_layers(layers, nl):

@@ -84,15 +84,17 @@ class Plan:
         return cls(g, device, blob)
 
     @classmethod
-    def fp8_from_model(cls, model, device, calib=None):
+    def fp8_from_model(cls, model, device, calib=None, min_cout=None):
         """BASELINE configs[4]: the fp16 plan with every 1x1 stride-1 conv (the Detect head excepted) on
         OCP e4m3 weights (per-output-channel scales) and e4m3 activations (per-tensor power-of-two
         scales), through the block-scaled fp8 MFMA (csrc/conv_f8.hip).
 
         Activation scales come from calibration: the fp16 plan runs `calib` ([B,3,H,W] frames in [0,1];
         default: 2 seeded synthetic frames at the model's native size) and each fp8 op's input amax
-        sets xscale = 2**ceil(log2(amax / 448)), so the largest calibrated value still fits e4m3."""
-        from yv7.graph import fp8_candidates
+        sets xscale = 2**ceil(log2(amax / 448)), so the largest calibrated value still fits e4m3.
+        min_cout: which eligible 1x1 convs go fp8 (default yv7.graph.FP8_MIN_COUT; 0 = all of them)."""
+        from yv7.graph import FP8_MIN_COUT, fp8_candidates
+        min_cout = FP8_MIN_COUT if min_cout is None else min_cout
         base = cls.from_model(model, device, torch.float16)
         if calib is None:
             from yv7.synthetic import synthetic_frames
@@ -104,7 +106,7 @@ class Plan:
         z = torch.empty((B, N, base.no), dtype=torch.float32, device=base.device)
         base.forward_into(x, z)
         scales = {}
-        for i in fp8_candidates(base.graph):
+        for i in fp8_candidates(base.graph, min_cout):
             o = base.graph.ops[i]
             v = base.tensor_view(o['src'], B, H, W)[..., o['src_coff']:o['src_coff'] + o['cin']]
             amax = float(v.abs().max().float())
