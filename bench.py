@@ -311,7 +311,7 @@ def main():
                          'mfma_frac': round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4)},
             'detail': {'forward_ms_events': round(fwd_ms, 3), 'conv_ms_events': round(conv_ms, 3),
                        'mean_dets_per_image': round(count_mean, 1), 'rows_per_image': N,
-                       'profiled_forwards': nf, 'nms_overlapped_with_next_forward': pipeline, 'hip_graph': graph is not None, 'sub_batches': nsplit, 'streams': nstreams},
+                       'profiled_forwards': nf, 'nms_overlapped_with_next_forward': pipeline or nstreams > 1, 'hip_graph': graph is not None, 'sub_batches': nsplit, 'streams': nstreams},
         }
         if not a.no_cpu_baseline and world == 1:
             res['cpu_baseline'] = cpu_baseline(a.model, a.img, a.cpu_seconds, plan=plan, dev=dev)
