@@ -150,10 +150,11 @@ def main():
     # step on one stream.
     nstreams = 1 if (a.split > 1 or a.graph) else max(1, a.streams)   # --split / --graph: one batch in flight
     pipeline = not (a.no_pipeline or a.graph) and nstreams == 1
-    nbuf = nstreams if nstreams > 1 else (2 if pipeline else 1)
-    fstreams = [torch.cuda.Stream(dev) for _ in range(nstreams)] if nstreams > 1 else []
-    for s_ in fstreams:
-        s_.wait_stream(torch.cuda.current_stream(dev))   # the frames were written on the default stream
+    nbuf = 2 if pipeline else 1
+    runner = None
+    if nstreams > 1:   # yv7.runtime.Inflight: the library's serving schedule, S batches in flight
+        from yv7.runtime import Inflight
+        runner = Inflight(plan, B, H, W, streams=nstreams, post=ydist.gather_detections if distributed else None)
     zs = [torch.empty((B, N, plan.no), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     dets = [torch.empty((B, 300, 6), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     srcs = [torch.empty((B, 300), dtype=torch.int64, device=dev) for _ in range(nbuf)]
@@ -192,11 +193,8 @@ def main():
     def step():
         k = nstep[0] % nbuf
         nstep[0] += 1
-        if fstreams:
-            s_ = fstreams[k]
-            plan.forward_into(x, zs[k], rowbest=rowbests[k], stream=s_.cuda_stream, ws_slot=k)
-            with torch.cuda.stream(s_):
-                post(k)
+        if runner is not None:
+            runner.submit(x)
             return
         if not pipeline:
             forward(zs[k], rowbests[k])
@@ -274,7 +272,7 @@ def main():
     mean_launch_s = max(conv_ms / 1e3 / nconv, 1e-12)   # 0 only under --no-live-events
     achieved_gbs = (conv_bytes / nconv) / mean_launch_s / 1e9
     achieved_tf = (conv_flops / nconv) / mean_launch_s / 1e12
-    count_mean = float(cnt.float().mean().item())
+    count_mean = float((runner.cnt[0] if runner is not None else cnt).float().mean().item())
     traffic = None
     if a.model == 'yolov7' and B == 32 and H == 640 and a.dtype == 'f16' and os.path.exists(PMC_TRAFFIC):
         with open(PMC_TRAFFIC) as f:

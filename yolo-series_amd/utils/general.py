@@ -81,16 +81,19 @@ def box_iou(box1, box2):  # general.py:464-486
 
 
 class _NmsWorkspace:
-    """Device scratch for yv7_nms, grown on demand and reused across calls (per device)."""
+    """Device scratch for yv7_nms, grown on demand and reused across calls — one buffer per (device,
+    stream): calls on one stream are ordered, calls on different streams (several batches in flight)
+    may run concurrently and must not share scratch."""
 
     def __init__(self):
         self.buf = {}
 
-    def get(self, device, nbytes):
-        t = self.buf.get(device)
+    def get(self, device, nbytes, stream=0):
+        key = (device, stream)
+        t = self.buf.get(key)
         if t is None or t.numel() < nbytes:
             t = torch.empty(max(nbytes, 1), dtype=torch.uint8, device=device)
-            self.buf[device] = t
+            self.buf[key] = t
         return t
 
 
@@ -128,8 +131,8 @@ def nms_batched(prediction, conf_thres=0.25, iou_thres=0.45, classes=None, agnos
     L = _lib.lib()
     multi = int(bool(multi_label))
     nbytes = L.yv7_nms_workspace_bytes(B, N, no, multi, max_nms)
-    ws = _WS.get(dev, nbytes)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    ws = _WS.get(dev, nbytes, stream)
     with torch.cuda.device(dev):
         rc = L.yv7_nms(z.data_ptr(), rowbest.data_ptr() if rowbest is not None else None, B, N, no,
                        float(conf_thres), float(iou_thres), multi, int(bool(agnostic)),
@@ -167,8 +170,8 @@ def end2end(prediction, conf_thres=0.25, iou_thres=0.45, topk=100):
     cls = torch.empty((B, topk), dtype=torch.int32, device=dev)
     L = _lib.lib()
     nbytes = L.yv7_end2end_workspace_bytes(B, N, no, topk)
-    ws = _WS.get(dev, nbytes)
     stream = torch.cuda.current_stream(dev).cuda_stream
+    ws = _WS.get(dev, nbytes, stream)
     with torch.cuda.device(dev):
         rc = L.yv7_end2end(z.data_ptr(), B, N, no, float(conf_thres), float(iou_thres), topk, num.data_ptr(),
                            boxes.data_ptr(), scores.data_ptr(), cls.data_ptr(), ws.data_ptr(), ws.numel(), stream)
