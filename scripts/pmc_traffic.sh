@@ -8,6 +8,6 @@ mkdir -p $OUT
 cd /tmp && export TMPDIR=/tmp
 for c in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $c --output-format csv -d $OUT/pmc_$c -o run -- \
-    python3 $R/bench.py --steps 4 --warmup 2 --no-cpu-baseline > $OUT/pmc_$c.log 2>&1 || { echo "$c pass failed"; exit 1; }
+    python3 $R/bench.py --steps 4 --warmup 2 --no-cpu-baseline --streams 1 > $OUT/pmc_$c.log 2>&1 || { echo "$c pass failed"; exit 1; }
 done
 echo done
