@@ -56,6 +56,8 @@ def parse():
                     'on the forward\'s stream instead of overlapping it with the next batch\'s forward')
     ap.add_argument('--streams', type=int, default=3, help='batches in flight (measured on MI355X, bs32 yolov7: 1 -> 5.6k, 2 -> 6.2k, 3 -> 6.3k, 4 -> 6.1k img/s): batch k runs its forward + NMS on '
                     'HIP stream k %% S with its own workspace and buffers, so consecutive batches overlap')
+    ap.add_argument('--prio', default='', help='comma-separated HIP stream priorities of the --streams streams '
+                    '(measured: default 6.38k, -1,0,0 6.34k, -1,-1,0 6.23k img/s — equal priorities pack best)')
     ap.add_argument('--graph', action='store_true', help='replay the step as a HIP graph (measured: same speed '
                     'as eager launches on MI355X, the inter-kernel gaps are dependency drains, not launch cost)')
     return ap.parse_args()
@@ -154,7 +156,9 @@ def main():
     runner = None
     if nstreams > 1:   # yv7.runtime.Inflight: the library's serving schedule, S batches in flight
         from yv7.runtime import Inflight
-        runner = Inflight(plan, B, H, W, streams=nstreams, post=ydist.gather_detections if distributed else None)
+        prios = [int(v) for v in a.prio.split(',')] if a.prio else None
+        runner = Inflight(plan, B, H, W, streams=nstreams, post=ydist.gather_detections if distributed else None,
+                          priorities=prios)
     zs = [torch.empty((B, N, plan.no), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     dets = [torch.empty((B, 300, 6), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     srcs = [torch.empty((B, 300), dtype=torch.int64, device=dev) for _ in range(nbuf)]

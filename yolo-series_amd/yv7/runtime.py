@@ -285,7 +285,8 @@ class Inflight:
         det, src_row, count = run.result(h)   # waits for that batch only; valid until S more submits
     """
 
-    def __init__(self, plan, B, H, W, streams=3, conf_thres=0.25, iou_thres=0.45, max_det=300, post=None):
+    def __init__(self, plan, B, H, W, streams=3, conf_thres=0.25, iou_thres=0.45, max_det=300, post=None,
+                 priorities=None):
         self.plan, self.S = plan, max(1, int(streams))
         self.conf, self.iou, self.max_det, self.post = conf_thres, iou_thres, max_det, post
         dev = plan.device
@@ -294,7 +295,8 @@ class Inflight:
             L.check(-2, f'yv7_num_rows(H={H}, W={W})')
         self.shape = (B, 3, H, W)
         S = self.S
-        self.streams = [torch.cuda.Stream(dev) for _ in range(S)]
+        prios = list(priorities) if priorities is not None else [0] * S   # HIP stream priorities (-1 = high)
+        self.streams = [torch.cuda.Stream(dev, priority=prios[i % len(prios)]) for i in range(S)]
         self.z = [torch.empty((B, N, plan.no), dtype=torch.float32, device=dev) for _ in range(S)]
         self.rowbest = [torch.empty((B, N, 4), dtype=torch.float32, device=dev) for _ in range(S)]
         self.det = [torch.empty((B, max_det, 6), dtype=torch.float32, device=dev) for _ in range(S)]
