@@ -276,6 +276,12 @@ def main():
     mean_launch_s = max(conv_ms / 1e3 / nconv, 1e-12)   # 0 only under --no-live-events
     achieved_gbs = (conv_bytes / nconv) / mean_launch_s / 1e9
     achieved_tf = (conv_flops / nconv) / mean_launch_s / 1e12
+    # whole-job ceiling: SURVEY §8d's canonical layer-boundary bytes per image (reference module boundaries,
+    # weights once per batch) at 8 TB/s; other configs: the plan's own op costs (which already credit the
+    # sibling-GEMM merges, so they slightly overstate that ceiling)
+    canon = {('yolov7', 640, 'f16'): 453.9e6, ('yolov7', 640, 'fp8'): 452.8e6, ('yolov7-w6', 1280, 'f16'): 1161.9e6}
+    img_bytes = canon.get((a.model, H, a.dtype), sum(by for _, _, by in costs) / B)
+    job_ceiling = HBM_PEAK_GBS * 1e9 / img_bytes   # images/s per GPU
     count_mean = float((runner.cnt[0] if runner is not None else cnt).float().mean().item())
     traffic = None
     if a.model == 'yolov7' and B == 32 and H == 640 and a.dtype == 'f16' and os.path.exists(PMC_TRAFFIC):
@@ -310,7 +316,11 @@ def main():
                          'launches_per_forward': nconv, 'mean_launch_us': round(mean_launch_s * 1e6, 2),
                          'algorithmic_bytes_per_launch': round(conv_bytes / nconv),
                          'mfma_tflops': round(achieved_tf, 1),
-                         'mfma_frac': round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4)},
+                         'mfma_frac': round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4),
+                         # whole job: images/s against the layer-boundary HBM ceiling of the whole forward
+                         # (17 625 img/s for yolov7 640 bs32 fp16)
+                         'job_ceiling_images_per_s': round(job_ceiling, 1),
+                         'job_frac': round(value / world / job_ceiling, 4)},
             'detail': {'forward_ms_events': round(fwd_ms, 3), 'conv_ms_events': round(conv_ms, 3),
                        'mean_dets_per_image': round(count_mean, 1), 'rows_per_image': N,
                        'profiled_forwards': nf, 'nms_overlapped_with_next_forward': pipeline or nstreams > 1, 'hip_graph': graph is not None, 'sub_batches': nsplit, 'streams': nstreams},
