@@ -1101,11 +1101,12 @@ Choice choose(const ConvParams& p, bool det) {
     // 88 -> 82, 1x1 256->256 @80 70 -> 61, 2048->512 @20 40 -> 37); the narrowest 1x1 take 128 x 64
     // (512->256 @20 11.7 -> 10.5); deep-K 3x3 layers under one round of tiles split K in two
     // (256->256 @20 35 -> 30, 512->256 @20 65 -> 47, s2 256->256 @40 36 -> 30; sc1 hand-off,
-    // splitk_reduce).  Wider grids keep the tuned wide tiles below.
+    // splitk_reduce), in four when a round of tiles covers at most half the CUs.  Wider grids keep the tuned wide tiles below.
     const long t128 = ring_tiles(p, R128x128s2);
     if (p.k > 1) {
       if (t128 <= 400) c.cfg = R128x128s2;
       if (t128 <= 256 && nk >= 36) c.S = 2;
+      if (t128 <= 128 && nk >= 36) c.S = 4;   // yolov7-w6 bs 8, 512->512 @20: 100 tiles x 4 K parts
     } else {
       if (t128 <= 400 || (p.K <= 256 && t128 <= 3200)) c.cfg = R128x128s2;
       if (t128 <= 200 && p.cout <= 256) c.cfg = R128x64;
@@ -1178,10 +1179,13 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // CU (1x1 128->128 @160 110 -> 89, 256->128 @160 161 -> 131, 256->256 @80 61 -> 55, 3x3
     // 128->128 @80 86 -> 81, s2 128->128 @160 96 -> 90, 512->512 @20 80 -> 76).
     const long t256 = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
+    const long t128 = (long)((p.M + 127) / 128) * ((p.cout + 127) / 128);
     if (one) {
       if (p.K >= 256 && p.cout >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
       if (p.K <= 512 && p.M >= 51200) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
-    } else if (p.k == 3 && (p.cout == 128 || (p.cout == 512 && p.Ho <= 20))) {
+    } else if (p.k == 3 && (p.cout == 128 || (p.cout == 512 && p.Ho <= 20 && t128 >= 256))) {
+      // (512->512 @20 with fewer 128 x 128 tiles than CUs — yolov7-w6 at bs 8: 100 tiles — goes to the
+      // split-K ring below instead: 72 us at 210 TF/s on 100 persistent blocks)
       return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     }
   }
