@@ -1106,7 +1106,10 @@ Choice choose(const ConvParams& p, bool det) {
     if (p.k > 1) {
       if (t128 <= 400) c.cfg = R128x128s2;
       if (t128 <= 256 && nk >= 36) c.S = 2;
-      if (t128 <= 128 && nk >= 36) c.S = 4;   // yolov7-w6 bs 8, 512->512 @20: 100 tiles x 4 K parts
+      static const long s4max = [] { const char* e = getenv("YV7_SPLIT4_TILES"); return e ? atol(e) : 128L; }();
+      // yolov7-w6 bs 8, 512->512 @20: 100 tiles x 4 K parts (72 -> 35 us); at 200 tiles (yolov7 bs 32,
+      // 256->256 @20) four parts lose to two: 33 -> 46 us (YV7_SPLIT4_TILES=256 A/B)
+      if (t128 <= s4max && nk >= 36) c.S = 4;
     } else {
       if (t128 <= 400 || (p.K <= 256 && t128 <= 3200)) c.cfg = R128x128s2;
       if (t128 <= 200 && p.cout <= 256) c.cfg = R128x64;
