@@ -74,9 +74,10 @@ def test_forward_fp32_full_size(name, B, H, W):
     print('\n' + check_z(z, zr, z64, f'{name} @{H}'))
 
 
-def test_forward_fp16_layerwise_scale():
-    """fp16 plan (the bench path): every layer within fp16 precision of the fp32 oracle (rms)."""
-    name, B, H, W = 'yolov7', 2, 128, 128
+@pytest.mark.parametrize('name,B,H,W', [('yolov7', 2, 128, 128), ('yolov7-w6', 1, 256, 320)])
+def test_forward_fp16_layerwise_scale(name, B, H, W):
+    """fp16 plan (the bench path): every layer within fp16 precision of the fp32 oracle (rms).  Small
+    frames put the deep 3x3 layers on the split-K ring (two and four K parts)."""
     x = frames(B, H, W, seed=5)
     zr, xsr, outs = _oracle(name, x)
     m = fresh_model(name).to(DEV).half()
@@ -92,7 +93,7 @@ def test_forward_fp16_layerwise_scale():
         rms = ref.pow(2).mean().sqrt().item()
         err = (got - ref).pow(2).mean().sqrt().item() / max(rms, 1e-3)
         worst = max(worst, err)
-    print(f'\nfp16: worst layer rms-rel err {worst:.3g}')
+    print(f'\n{name} fp16: worst layer rms-rel err {worst:.3g}')
     assert worst < 0.05
 
 
