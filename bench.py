@@ -39,7 +39,7 @@ MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument('--gpus', type=int, default=1)
-    ap.add_argument('--steps', type=int, default=20)
+    ap.add_argument('--steps', type=int, default=60)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--batch', type=int, default=32, help='images per GPU')
     ap.add_argument('--img', type=int, default=640)
