@@ -46,6 +46,8 @@ def parse():
     ap.add_argument('--model', default='yolov7')
     ap.add_argument('--dtype', default='f16', choices=['f16', 'f32', 'fp8'],
                     help='fp8: BASELINE configs[4] (1x1 convs on e4m3 weights/activations, fp16 elsewhere)')
+    ap.add_argument('--fp8-min-cout', type=int, default=None, help='fp8: narrowest 1x1 conv run in e4m3 '
+                    '(default yv7.graph.FP8_MIN_COUT; 0 = every eligible 1x1)')
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='bounded CPU-baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-live-events', action='store_true', help='diagnostic: time the steps without per-op HIP events')
@@ -136,7 +138,7 @@ def main():
         synthetic_state_dict(model, seed=0)
         model = model.float().fuse().eval()
     if a.dtype == 'fp8':   # every rank calibrates its own fp8 plan (deterministic: same frames, same scales)
-        plan = Plan.from_model(model, dev, 'fp8')
+        plan = Plan.fp8_from_model(model, dev, min_cout=a.fp8_min_cout)
     elif distributed:
         plan = ydist.broadcast_weights(model, dev, dt)
     else:
