@@ -1182,7 +1182,6 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // CU (1x1 128->128 @160 110 -> 89, 256->128 @160 161 -> 131, 256->256 @80 61 -> 55, 3x3
     // 128->128 @80 86 -> 81, s2 128->128 @160 96 -> 90, 512->512 @20 80 -> 76).
     const long t256 = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
-    const long t128 = (long)((p.M + 127) / 128) * ((p.cout + 127) / 128);
     // Wide layers with at least 200 tiles of 256 x 256 (in-network sweep of every ring configuration,
     // yolov7 bs 32, us, default -> persistent 256 x 256): 1x1 1024->1024 @40 156 -> 135, 1024->512 @40
     // 79 -> 69, 512->512 @40 55 -> 48, 1024->1024 @20 44 -> 39; 3x3 256->256 @40 86 -> 70, s2 256->256
@@ -1193,14 +1192,12 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
       if (p.K >= 256 && p.cout >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
       if (wide && p.cout >= 256 && t256 >= 200) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
       if (p.K <= 512 && p.M >= 51200) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
-    } else if (wide && p.k == 3 && p.cout == 512 && p.Ho <= 20 && t128 >= 256) {
-      // 3x3 512->512 @20 (and s2 from @40): 256 x 128 persistent ring, 92 -> 83 us
-      return launch_pring<256, 128, 4, 2, 3>(p, one, 1, st);
     } else if (wide && p.k == 3 && p.cin >= 256 && p.cout >= 256 && t256 >= 200) {
       return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
-    } else if (p.k == 3 && (p.cout == 128 || (p.cout == 512 && p.Ho <= 20 && t128 >= 256))) {
-      // (512->512 @20 with fewer 128 x 128 tiles than CUs — yolov7-w6 at bs 8: 100 tiles — goes to the
-      // split-K ring below instead: 72 us at 210 TF/s on 100 persistent blocks)
+    } else if (p.k == 3 && p.cout == 128) {
+      // (3x3 512->512 @20 and s2 from @40 take the non-persistent 128 x 128 ring of choose() below:
+      // in-network 92 (this ring) / 89 (256 x 128 persistent) -> 79 us; with fewer tiles than CUs,
+      // yolov7-w6 at bs 8, it splits K: 72 -> 35 us)
       return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     }
   }
