@@ -60,6 +60,8 @@ def parse():
                     'HIP stream k %% S with its own workspace and buffers, so consecutive batches overlap')
     ap.add_argument('--prio', default='', help='comma-separated HIP stream priorities of the --streams streams '
                     '(measured: default 6.38k, -1,0,0 6.34k, -1,-1,0 6.23k img/s — equal priorities pack best)')
+    ap.add_argument('--h2d', action='store_true', help='diagnostic, never `value` of the headline: upload each '
+                    'batch as uint8 frames from pinned host memory (PCIe-inclusive rate)')
     ap.add_argument('--graph', action='store_true', help='replay the step as a HIP graph (measured: same speed '
                     'as eager launches on MI355X, the inter-kernel gaps are dependency drains, not launch cost)')
     return ap.parse_args()
@@ -155,6 +157,14 @@ def main():
     nstreams = 1 if (a.split > 1 or a.graph) else max(1, a.streams)   # --split / --graph: one batch in flight
     pipeline = not (a.no_pipeline or a.graph) and nstreams == 1
     nbuf = 2 if pipeline else 1
+    h2d = None
+    if a.h2d:   # PCIe-inclusive rate: pinned uint8 host frames uploaded every step
+        if nstreams < 2:
+            raise SystemExit('--h2d runs on the batches-in-flight schedule (--streams >= 2)')
+        host = torch.randint(0, 256, (B, 3, H, W), generator=torch.Generator().manual_seed(1000 + rank),
+                             dtype=torch.uint8).pin_memory()
+        h2d = {'host': host, 'u8': [torch.empty((B, 3, H, W), dtype=torch.uint8, device=dev) for _ in range(nstreams)],
+               'x': [torch.empty((B, 3, H, W), dtype=dt, device=dev) for _ in range(nstreams)]}
     runner = None
     if nstreams > 1:   # yv7.runtime.Inflight: the library's serving schedule, S batches in flight
         from yv7.runtime import Inflight
@@ -200,7 +210,19 @@ def main():
         k = nstep[0] % nbuf
         nstep[0] += 1
         if runner is not None:
-            runner.submit(x)
+            if h2d is None:
+                runner.submit(x)
+                return
+            # --h2d: this batch's uint8 frames come from pinned host memory (detect.py:100-104 hands the
+            # model host frames): upload + /255 on the default stream, ordered after the forward that
+            # last read this slot's device frames
+            j = runner.n % nstreams          # the slot this submission will use
+            cur = torch.cuda.current_stream(dev)
+            if runner.n >= nstreams:
+                cur.wait_event(runner.done[j])
+            h2d['u8'][j].copy_(h2d['host'], non_blocking=True)
+            torch.div(h2d['u8'][j], 255.0, out=h2d['x'][j])
+            runner.submit(h2d['x'][j])
             return
         if not pipeline:
             forward(zs[k], rowbests[k])
@@ -325,7 +347,7 @@ def main():
                          'job_frac': round(value / world / job_ceiling, 4)},
             'detail': {'forward_ms_events': round(fwd_ms, 3), 'conv_ms_events': round(conv_ms, 3),
                        'mean_dets_per_image': round(count_mean, 1), 'rows_per_image': N,
-                       'profiled_forwards': nf, 'nms_overlapped_with_next_forward': pipeline or nstreams > 1, 'hip_graph': graph is not None, 'sub_batches': nsplit, 'streams': nstreams},
+                       'profiled_forwards': nf, 'nms_overlapped_with_next_forward': pipeline or nstreams > 1, 'hip_graph': graph is not None, 'sub_batches': nsplit, 'streams': nstreams, 'h2d_uint8_frames': bool(a.h2d)},
         }
         if not a.no_cpu_baseline and world == 1:
             res['cpu_baseline'] = cpu_baseline(a.model, a.img, a.cpu_seconds, plan=plan, dev=dev)
