@@ -36,9 +36,12 @@ PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r1_pmc_traffic.json')
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA
 
 
-def parse():
+def parse(argv=None):
     ap = argparse.ArgumentParser()
-    ap.add_argument('--gpus', type=int, default=1)
+    ap.add_argument('--gpus', type=int, default=1, help='ranks (one process per GPU); without an outer '
+                    'torch.distributed.run, bench.py starts one itself')
+    ap.add_argument('--plumbing', action='store_true', help='CPU check of the multi-rank path only (gloo, no '
+                    'GPU, no timing): launcher, weight-blob broadcast, detection all-gather, world size')
     ap.add_argument('--steps', type=int, default=60)
     ap.add_argument('--warmup', type=int, default=5)
     ap.add_argument('--batch', type=int, default=32, help='images per GPU')
@@ -51,6 +54,8 @@ def parse():
     ap.add_argument('--cpu-seconds', type=float, default=12.0, help='bounded CPU-baseline sample')
     ap.add_argument('--no-cpu-baseline', action='store_true')
     ap.add_argument('--no-live-events', action='store_true', help='diagnostic: time the steps without per-op HIP events')
+    ap.add_argument('--live-forwards', type=int, default=3, help='timed forwards that record per-op HIP events '
+                    '(the roofline\'s per-launch durations)')
     ap.add_argument('--split', type=int, default=1, help='run the batch as this many concurrent sub-batches, '
                     'each on its own HIP stream and workspace (fills the low-resolution layers\' tails and the '
                     'kernel-boundary gaps of one stream with the other\'s work)')
@@ -64,11 +69,88 @@ def parse():
                     'batch as uint8 frames from pinned host memory (PCIe-inclusive rate)')
     ap.add_argument('--graph', action='store_true', help='replay the step as a HIP graph (measured: same speed '
                     'as eager launches on MI355X, the inter-kernel gaps are dependency drains, not launch cost)')
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
-def cpu_baseline(model_name, img, seconds, plan=None, dev=None, parity_frames=4):
-    """The oracle (reference CPU path restated) on host cores: forward + NMS per frame, batch 1.
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(a, argv):
+    """--gpus N > 1 without an outer launcher: start N ranks with torch.distributed.run as a CHILD
+    process (this process has not touched the GPU; it never execs) and return its exit code."""
+    import subprocess
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1', f'--nproc-per-node={a.gpus}',
+           '--master-addr=127.0.0.1', f'--master-port={_free_port()}', os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get('HSA_ENABLE_IPC_MODE_LEGACY', '0'))
+    return subprocess.call(cmd, env=env)
+
+
+def plumbing(a):
+    """The N > 1 data path on CPU ranks (gloo): the same yv7.dist calls the GPU ranks make, minus the
+    kernels.  Prints one JSON line with the world size the process group saw."""
+    dist.init_process_group('gloo')
+    world, rank = dist.get_world_size(), dist.get_rank()
+    if world != a.gpus:
+        raise SystemExit(f'--gpus {a.gpus} but the process group has {world} ranks')
+    from models.yolo import Model
+    from yv7 import _lib as L
+    from yv7 import dist as ydist
+    from yv7.graph import compile_model
+    from yv7.synthetic import synthetic_state_dict
+    import contextlib
+    with contextlib.redirect_stdout(sys.stderr):
+        model = Model(a.model)
+        synthetic_state_dict(model, seed=0)
+        model = model.float().fuse().eval()
+    g = compile_model(model, L.DT_F16)
+    blob = ydist.broadcast_blob(g, torch.device('cpu'))
+    same = torch.equal(blob, g.weight_blob())
+    lo, hi = ydist.shard(a.batch * world, rank, world)
+    b = hi - lo
+    det = torch.full((b, 300, 6), float(rank))
+    src = torch.full((b, 300), rank, dtype=torch.int64)
+    cnt = torch.arange(lo, hi, dtype=torch.int32)
+    gd, gs, gc = ydist.gather_detections(det, src, cnt)
+    ok = same and gc.tolist() == list(range(a.batch * world)) and gd.shape[0] == a.batch * world
+    flags = torch.tensor([int(ok)])
+    dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    if rank == 0:
+        print(json.dumps({'plumbing': True, 'n_gpus': world, 'world_size_seen': world, 'backend': 'gloo',
+                          'weights_broadcast_bytes': int(blob.numel()), 'global_batch': a.batch * world,
+                          'all_ranks_ok': bool(flags.item())}), flush=True)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def _cpu_model():
+    try:
+        for line in open('/proc/cpuinfo'):
+            if line.startswith('model name'):
+                return line.split(':', 1)[1].strip()
+    except OSError:
+        pass
+    return 'unknown'
+
+
+def _cpu_quota():
+    """CPUs the job's cgroup allows (cpu.max), or None."""
+    try:
+        q, per = open('/sys/fs/cgroup/cpu.max').read().split()[:2]
+        return None if q == 'max' else round(int(q) / int(per), 2)
+    except (OSError, ValueError):
+        return None
+
+
+def cpu_baseline(model_name, img, seconds, plan=None, dev=None, parity_frames=4, big_batch=32):
+    """The oracle (reference CPU path restated) on the host cores this job may use: forward + NMS,
+    timed separately like detect.py:142-153 (t2 - t1 forward, t3 - t2 NMS), at batch 1 (detect.py's
+    loop; `value`) for about `seconds`, and one batch of `big_batch` frames (test.py's batch size).
 
     Also the metric's parity half: on `parity_frames` synthetic frames the oracle's fp32 detections
     (detect.py settings, conf 0.25 / iou 0.45) are the ground truth for the GPU fp16 plan's
@@ -76,26 +158,42 @@ def cpu_baseline(model_name, img, seconds, plan=None, dev=None, parity_frames=4)
     from oracle import nms_ref, yolo_ref
     from models.yolo import Model
     from yv7.synthetic import synthetic_frames, synthetic_state_dict
-    threads = min(16, os.cpu_count() or 1)
-    torch.set_num_threads(threads)
+    threads = torch.get_num_threads()   # OMP_NUM_THREADS / the job's CPU share: every core it may use
     m = Model(model_name)
     sd = synthetic_state_dict(m, seed=0)
     net = yolo_ref.parse(m.yaml)
     fused = yolo_ref.fuse(net, sd)
-    x = synthetic_frames(1, img, img, seed=1)
-    with torch.no_grad():
-        z, _ = yolo_ref.forward(net, fused, x)  # warm-up
-        n, t0 = 0, time.time()
+
+    def run(x, min_s, min_n):
+        t_fwd = t_nms = 0.0
+        n = 0
         while True:
+            t1 = time.perf_counter()
             z, _ = yolo_ref.forward(net, fused, x)
+            t2 = time.perf_counter()
             nms_ref.non_max_suppression(z, 0.25, 0.45)
+            t3 = time.perf_counter()
+            t_fwd += t2 - t1
+            t_nms += t3 - t2
             n += 1
-            if time.time() - t0 >= seconds and n >= 2:
-                break
-        dt = time.time() - t0
-    out = {'value': round(n / dt, 3), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
-           'sample': f'{n} frames of {model_name} {img}x{img}, batch 1, fp32 NCHW, forward + NMS '
-                     f'(conf 0.25, iou 0.45), {dt:.1f} s, torch {torch.__version__} CPU'}
+            if t_fwd + t_nms >= min_s and n >= min_n:
+                return n, t_fwd, t_nms
+
+    with torch.no_grad():
+        x1 = synthetic_frames(1, img, img, seed=1)
+        yolo_ref.forward(net, fused, x1)  # warm-up
+        n1, f1, s1 = run(x1, seconds, 2)
+        xb = synthetic_frames(big_batch, img, img, seed=2)
+        nb, fb, sb = run(xb, 0.0, 1)
+    out = {'value': round(n1 / (f1 + s1), 3), 'unit': 'images/sec', 'cores': threads, 'kind': 'port',
+           'sample': f'{n1} frames of {model_name} {img}x{img}, batch 1, fp32 NCHW, forward + NMS '
+                     f'(conf 0.25, iou 0.45), {f1 + s1:.1f} s; then {nb} batch(es) of {big_batch}; '
+                     f'torch {torch.__version__} CPU, {threads} threads',
+           'cpu': _cpu_model(), 'machine_cpus': os.cpu_count(), 'cgroup_cpus': _cpu_quota(),
+           'batch1': {'images_per_s': round(n1 / (f1 + s1), 3), 'forward_ms': round(f1 / n1 * 1e3, 1),
+                      'nms_ms': round(s1 / n1 * 1e3, 2)},
+           f'batch{big_batch}': {'images_per_s': round(nb * big_batch / (fb + sb), 3),
+                                 'forward_ms': round(fb / nb * 1e3, 1), 'nms_ms': round(sb / nb * 1e3, 2)}}
     if plan is not None and parity_frames > 0:
         from utils.general import nms_batched
         from utils.metrics import dets_as_labels, map_from_lists
@@ -115,14 +213,23 @@ def cpu_baseline(model_name, img, seconds, plan=None, dev=None, parity_frames=4)
     return out
 
 
-def main():
-    a = parse()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    if 'WORLD_SIZE' not in os.environ and a.gpus > 1:
+        sys.exit(launch_ranks(a, argv))
+    if a.plumbing:
+        return plumbing(a)
     world = int(os.environ.get('WORLD_SIZE', '1'))
     rank = int(os.environ.get('RANK', '0'))
     local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world != a.gpus:
+        raise SystemExit(f'--gpus {a.gpus} but WORLD_SIZE={world}')
     distributed = world > 1
     if distributed:
         dist.init_process_group('nccl', device_id=torch.device(f'cuda:{local}'))
+        if dist.get_world_size() != a.gpus:
+            raise SystemExit(f'--gpus {a.gpus} but RCCL sees {dist.get_world_size()} ranks')
     torch.cuda.set_device(local)
     dev = torch.device(f'cuda:{local}')
 
@@ -197,7 +304,7 @@ def main():
             s_.wait_stream(main)
         for i, s_ in enumerate(streams):
             sl = slice(i * sub, (i + 1) * sub)
-            plan.forward_into(x[sl], z[sl], rowbest=rowbest[sl], stream=s_.cuda_stream, ws_slot=i)
+            plan.forward_into(x[sl], z[sl], rowbest=rowbest[sl], stream=s_, ws_slot=i)
         for s_ in streams[1:]:
             main.wait_stream(s_)
 
@@ -257,16 +364,18 @@ def main():
             step()
         graph.replay()
         torch.cuda.synchronize()
-    # with --split the per-op events would time overlapping kernels of two streams: they are taken on
-    # two whole-batch forwards after the timed steps instead
-    n_live = 0 if (a.no_live_events or nsplit > 1 or nstreams > 1) else min(a.steps, 2)
+    # Live per-op HIP events inside the timed region: libyv7's profile mode records an event before the
+    # first op and after every op of the first n_live timed forwards, on the stream each forward runs on
+    # (with batches in flight the three streams' kernels share the chip, so these are the durations of the
+    # timed regime, contention included).  Not under --graph / --split.
+    n_live = 0 if (a.no_live_events or nsplit > 1 or graph is not None) else min(a.steps, a.live_forwards)
     plan.profile_enable(n_live)
     if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for i in range(a.steps):
-        if graph is None or i < n_live:
+        if graph is None:
             step()
         else:
             graph.replay()
@@ -279,27 +388,48 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
 
-    if (nsplit > 1 or nstreams > 1) and not a.no_live_events:
-        plan.profile_enable(2)
-        for _ in range(2):
-            plan.forward_into(x, z, rowbest=rowbest)
-        torch.cuda.synchronize()
-    nf, op_ms = plan.profile_read()
-    plan.profile_enable(0)
-    costs = plan.op_costs(B, H, W, x_bytes=x.element_size(), with_raw=False)
     from yv7 import _lib as L
-    conv_ms = conv_bytes = conv_flops = 0.0
-    nconv = 0
-    fwd_ms = sum(op_ms) / max(nf, 1)
-    for (kind, fl, by), ms in zip(costs, op_ms):
-        if kind in (L.OP_CONV, L.OP_DETECT):
-            conv_ms += ms / max(nf, 1)
-            conv_bytes += by
-            conv_flops += fl
-            nconv += 1
-    mean_launch_s = max(conv_ms / 1e3 / nconv, 1e-12)   # 0 only under --no-live-events
-    achieved_gbs = (conv_bytes / nconv) / mean_launch_s / 1e9
-    achieved_tf = (conv_flops / nconv) / mean_launch_s / 1e12
+    costs = plan.op_costs(B, H, W, x_bytes=x.element_size(), with_raw=False)
+
+    def conv_family(nf, op_ms):
+        """(mean conv/DETECT launch s, bytes per launch, flops per launch, launches, forward ms, conv ms)."""
+        conv_ms = conv_bytes = conv_flops = 0.0
+        nconv = 0
+        for (kind, fl, by), ms in zip(costs, op_ms):
+            if kind in (L.OP_CONV, L.OP_DETECT):
+                conv_ms += ms / max(nf, 1)
+                conv_bytes += by
+                conv_flops += fl
+                nconv += 1
+        return (max(conv_ms / 1e3 / nconv, 1e-12), conv_bytes / nconv, conv_flops / nconv, nconv,
+                sum(op_ms) / max(nf, 1), conv_ms)
+
+    nf, op_ms = plan.profile_read()
+    timed = conv_family(nf, op_ms)
+    # Diagnostics after the timed region (never `value`): two serial forwards with per-op events (each
+    # kernel alone on the chip), then detect.py's split (detect.py:142-153): forward and NMS timed apart
+    # with HIP events on one stream, one batch at a time.
+    plan.profile_enable(2)
+    for _ in range(2):
+        plan.forward_into(x, z, rowbest=rowbest)
+    torch.cuda.synchronize()
+    nf_s, op_ms_s = plan.profile_read()
+    plan.profile_enable(0)
+    serial = conv_family(nf_s, op_ms_s)
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
+    f_ms = n_ms = 0.0
+    for _ in range(3):
+        ev[0].record()
+        plan.forward_into(x, z, rowbest=rowbest)
+        ev[1].record()
+        nms_batched(z, 0.25, 0.45, out=(det, src, cnt), rowbest=rowbest)
+        ev[2].record()
+        ev[2].synchronize()
+        f_ms += ev[0].elapsed_time(ev[1]) / 3
+        n_ms += ev[1].elapsed_time(ev[2]) / 3
+    mean_launch_s, bytes_per_launch, flops_per_launch, nconv, fwd_ms, conv_ms = timed if nf else serial
+    achieved_gbs = bytes_per_launch / mean_launch_s / 1e9
+    achieved_tf = flops_per_launch / mean_launch_s / 1e12
     # whole-job ceiling: SURVEY §8d's canonical layer-boundary bytes per image (reference module boundaries,
     # weights once per batch) at 8 TB/s; other configs: the plan's own op costs (which already credit the
     # sibling-GEMM merges, so they slightly overstate that ceiling)
@@ -331,6 +461,7 @@ def main():
                                    f'(conf 0.25, iou 0.45, max_det 300)'
                                    + (' + RCCL all-gather of detections' if distributed else ''),
                        'global_batch': world * B, 'img': H, 'parallelism': f'dp{world}',
+                       'rccl_world_size': dist.get_world_size() if distributed else 1,
                        'weights': 'seeded synthetic, RCCL-broadcast' if distributed else 'seeded synthetic'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved_gbs / HBM_PEAK_GBS, 4), 'traffic': traffic,
@@ -338,7 +469,10 @@ def main():
                          'kernel': 'conv kernels (MFMA implicit-GEMM ring / persistent ring / weight-stationary '
                                    '3x3 / halo; all CONV and DETECT launches of the forward)',
                          'launches_per_forward': nconv, 'mean_launch_us': round(mean_launch_s * 1e6, 2),
-                         'algorithmic_bytes_per_launch': round(conv_bytes / nconv),
+                         'timing': (f'HIP events around every op of {nf} forwards inside the timed region, on '
+                                    f'each forward\'s stream ({nstreams} stream(s) in flight)') if nf else
+                                   'HIP events around every op of 2 serial forwards after the timed region',
+                         'algorithmic_bytes_per_launch': round(bytes_per_launch),
                          'mfma_tflops': round(achieved_tf, 1),
                          'mfma_frac': round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4),
                          # whole job: images/s against the layer-boundary HBM ceiling of the whole forward
@@ -346,6 +480,13 @@ def main():
                          'job_ceiling_images_per_s': round(job_ceiling, 1),
                          'job_frac': round(value / world / job_ceiling, 4)},
             'detail': {'forward_ms_events': round(fwd_ms, 3), 'conv_ms_events': round(conv_ms, 3),
+                       'serial_conv_launch_us': round(serial[0] * 1e6, 2),
+                       'serial_conv_frac': round(serial[1] / serial[0] / 1e9 / HBM_PEAK_GBS, 4),
+                       'serial_conv_tflops': round(serial[2] / serial[0] / 1e12, 1),
+                       'serial_forward_ms': round(serial[4], 3),
+                       'detect_py_split_ms': {'forward': round(f_ms, 3), 'nms': round(n_ms, 3),
+                                              'note': 'one batch at a time on one stream, HIP events '
+                                                      '(detect.py:142-153 t2-t1 / t3-t2)'},
                        'mean_dets_per_image': round(count_mean, 1), 'rows_per_image': N,
                        'profiled_forwards': nf, 'nms_overlapped_with_next_forward': pipeline or nstreams > 1, 'hip_graph': graph is not None, 'sub_batches': nsplit, 'streams': nstreams, 'h2d_uint8_frames': bool(a.h2d)},
         }

@@ -35,8 +35,11 @@ extern "C" {
 
 /* Activation tensors in the forward workspace are NHWC with a YV7_BORDER-pixel zero frame around
  * every image: [B][h + 2*YV7_BORDER][w + 2*YV7_BORDER][C].  Kernels write only interiors; the frame
- * serves every 3x3 / pad-1 window's out-of-image taps.  yv7_forward clears the workspace the first
- * time it sees it (pointer and size), so between calls the workspace must belong to that plan. */
+ * serves every 3x3 / pad-1 window's out-of-image taps.  yv7_forward clears a workspace the first
+ * time it sees it with a given layout (pointer, size and batch geometry B, H, W) and trusts the frame
+ * on later calls with that layout.  So between calls the workspace memory belongs to the plan: a
+ * caller that frees it, reuses it for anything else or writes into it calls yv7_workspace_forget
+ * first (the Python binding does so whenever it drops a workspace). */
 #define YV7_BORDER 1
 
 typedef enum {
@@ -116,6 +119,9 @@ void yv7_plan_destroy(yv7_plan* plan);
 
 /* Bytes of caller-provided workspace yv7_forward needs for a [B,3,H,W] batch. */
 size_t yv7_workspace_bytes(const yv7_plan* plan, int B, int H, int W);
+/* Hand workspace memory [ws, ws + bytes) back to the caller: the next yv7_forward on any part of it
+ * clears it again. */
+int yv7_workspace_forget(yv7_plan* plan, const void* ws, size_t bytes);
 /* Rows of z per image: sum over levels of na * (H >> s_l) * (W >> s_l). */
 int64_t yv7_num_rows(const yv7_plan* plan, int H, int W);
 
@@ -136,6 +142,12 @@ typedef struct {
  * yv7_row_best (fp16 plans write it from the head's epilogue).  Asynchronous on `stream`. */
 int yv7_forward(yv7_plan* plan, const void* x, int x_dtype, int B, int H, int W, float* z_out,
                 float* raw_out, yv7_row_best* rowbest_out, void* workspace, size_t ws_bytes, void* stream);
+
+/* Force the kernel configuration of one CONV / DETECT op (0 = the tuned dispatch, the default).  For
+ * parity tests of every kernel variant and A/B timing; the accepted values are the real kernel
+ * configurations of the fp16 dispatch (csrc/conv_f16.hip), never its microbenchmark hooks.  A split-K
+ * variant changes yv7_workspace_bytes. */
+int yv7_set_op_variant(yv7_plan* plan, int op, int variant);
 
 /* Live per-op timing: with max_forwards > 0 every following yv7_forward (up to max_forwards of
  * them) records one HIP event before its first op and one after each op on its stream; 0 turns it

@@ -154,3 +154,45 @@ def scale_coords(img1_shape, coords, img0_shape):
     c[:, 2].clamp_(0, img0_shape[1])
     c[:, 3].clamp_(0, img0_shape[0])
     return c
+
+
+def end2end(prediction, conf_thres=0.25, iou_thres=0.45, topk=100, max_nms=65536):
+    """The End2End / EfficientNMS_TRT output contract (models/experimental.py:195-241, TRT_NMS
+    111-156; inf_onnx_trt.py:27-36 reads it): ONNX_TRT hands the plugin boxes = z[..., :4] (xywh,
+    box_coding 1) and scores = z[..., 5:] * z[..., 4:5] (z[..., 4:5] when nc == 1); the plugin keeps
+    every (box, class) with score > score_threshold, suppresses within a class only (no class
+    offset, background_class -1) where IoU > iou_threshold on the corner boxes, and returns the top
+    max_output_boxes by score: num_dets int32 [B,1], det_boxes [B,topk,4] xyxy, det_scores [B,topk],
+    det_classes int32 [B,topk], zero-padded.  The TensorRT plugin is not in the reference (nor this
+    image), so this restates its published algorithm; ties resolve like the rest of the oracle (stable
+    descending score order, candidates row-major then class) and at most max_nms candidates enter
+    the suppression.  Parity unpinned at the plugin boundary."""
+    z = prediction.detach().cpu().float()
+    B, N, no = z.shape
+    nc = no - 5
+    num = torch.zeros((B, 1), dtype=torch.int32)
+    boxes = torch.zeros((B, topk, 4))
+    scores = torch.zeros((B, topk))
+    classes = torch.zeros((B, topk), dtype=torch.int32)
+    for b in range(B):
+        x = z[b]
+        box = xywh2xyxy(x[:, :4])
+        sc = x[:, 4:5].clone() if nc == 1 else x[:, 5:] * x[:, 4:5]
+        i, j = (sc > conf_thres).nonzero(as_tuple=False).T
+        if not i.numel():
+            continue
+        s = sc[i, j]
+        o = torch.sort(s, descending=True, stable=True).indices[:max_nms]
+        i, j, s = i[o], j[o], s[o]
+        kept = []
+        for c in j.unique().tolist():
+            idx = (j == c).nonzero().view(-1)       # ascending = score order within the class
+            k = nms(box[i[idx]], s[idx], iou_thres)
+            kept.append(idx[k])
+        kept = torch.sort(torch.cat(kept)).values[:topk]   # back to the global score order
+        n = kept.numel()
+        num[b, 0] = n
+        boxes[b, :n] = box[i[kept]]
+        scores[b, :n] = s[kept]
+        classes[b, :n] = j[kept].to(torch.int32)
+    return num, boxes, scores, classes

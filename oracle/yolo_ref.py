@@ -12,6 +12,8 @@ This file restates, from the reference sources read as text (never imported or e
   * layer forwards              Conv.fuseforward common.py:110-111, RepConv deploy common.py:498-500,
                                 SPPCSPC common.py:276-280, MP 30-36, SP 39-45, ReOrg 48-53, Concat 56-62
   * Detect decode               models/yolo.py:42-63 (== IDetect.fuseforward 140-160)
+  * test-time augmentation      models/yolo.py:582-597 (+ scale_img utils/torch_utils.py:247-257)
+  * Ensemble                    models/experimental.py:69-81
 It is written as plain functions over a layer table and a reference-keyed state_dict, so the
 same synthetic weights can be fed to the product (models.yolo.Model.load_state_dict) and here.
 """
@@ -400,3 +402,42 @@ def forward64(net: Net, fused: dict, x: torch.Tensor):
     finally:
         net.anchor_grid = ag
     return z, xs
+
+
+def scale_img(img, ratio=1.0, same_shape=False, gs=32):  # utils/torch_utils.py:247-257
+    if ratio == 1.0:
+        return img
+    h, w = img.shape[2:]
+    s = (int(h * ratio), int(w * ratio))
+    img = F.interpolate(img, size=s, mode='bilinear', align_corners=False)
+    if not same_shape:
+        h, w = [math.ceil(x * ratio / gs) * gs for x in (h, w)]
+    return F.pad(img, [0, w - s[1], 0, h - s[0]], value=0.447)
+
+
+def forward_augment(net: Net, fused: dict, x: torch.Tensor, f64=False):
+    """Model.forward(augment=True) (models/yolo.py:582-597): three passes (scale 1, 0.83 with an lr
+    flip, 0.67), de-scaled / de-flipped boxes, rows concatenated.  f64: the float64 yardstick (the
+    input resizes in float64 too)."""
+    img_size = x.shape[-2:]
+    gs = int(max(net.stride))
+    if f64:
+        x = x.double()
+    y = []
+    for si, fi in zip([1, 0.83, 0.67], [None, 3, None]):
+        xi = scale_img(x.flip(fi) if fi else x, si, gs=gs)
+        yi = (forward64(net, fused, xi) if f64 else forward(net, fused, xi))[0]
+        yi[..., :4] /= si
+        if fi == 2:
+            yi[..., 1] = img_size[0] - yi[..., 1]
+        elif fi == 3:
+            yi[..., 0] = img_size[1] - yi[..., 0]
+        y.append(yi)
+    return torch.cat(y, 1)
+
+
+def ensemble_forward(members, x, f64=False):
+    """Ensemble.forward (models/experimental.py:74-81): each member's z, concatenated on the row axis
+    ("nms ensemble").  members: [(net, fused), ...]."""
+    fw = forward64 if f64 else forward
+    return torch.cat([fw(net, fused, x.double() if f64 else x)[0] for net, fused in members], 1)

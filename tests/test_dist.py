@@ -28,17 +28,18 @@ def _worker(rank, world, port, q):
     try:
         from models.yolo import Model
         from yv7 import _lib as L
-        from yv7.dist import gather_detections, shard
+        from yv7.dist import broadcast_blob, gather_detections, shard
         from yv7.graph import compile_model
         from yv7.synthetic import synthetic_state_dict
-        # every rank builds the same synthetic weights; rank 0's packed blob is broadcast
+        # every rank compiles the graph; only rank 0 packs, the blob reaches the others by broadcast
+        # (yv7.dist.broadcast_blob: the code broadcast_weights runs before creating each rank's plan)
         m = Model('yolov7-tiny')
-        synthetic_state_dict(m, seed=0)
+        synthetic_state_dict(m, seed=rank)     # rank 1's own weights differ: only the broadcast makes them equal
         g = compile_model(m.float().fuse(), L.DT_F16)
-        mine = g.weight_blob()
-        blob = mine.clone() if rank == 0 else torch.zeros_like(mine)
-        dist.broadcast(blob, src=0)
-        same_blob = torch.equal(blob, mine)
+        blob = broadcast_blob(g, torch.device('cpu'))
+        m0 = Model('yolov7-tiny')
+        synthetic_state_dict(m0, seed=0)
+        same_blob = torch.equal(blob, compile_model(m0.float().fuse(), L.DT_F16).weight_blob())
         # per-rank fixed-shape NMS outputs for its slice of a global batch of 6 images
         lo, hi = shard(6, rank, world)
         b = hi - lo
@@ -73,3 +74,22 @@ def test_gloo_world2_broadcast_and_gather():
     for rank, same_blob, d, s, c in res:
         assert same_blob
         assert d == [0, 1, 2, 3, 4, 5] and s == [0, 1, 2, 3, 4, 5] and c == [0, 1, 2, 3, 4, 5]
+
+
+def test_bench_launcher_starts_ranks():
+    """`bench.py --gpus 2` with no outer launcher starts two ranks itself (torch.distributed.run as a
+    child process) and the process group they form has world size 2 (--plumbing: the CPU/gloo form of
+    the multi-rank path: weight-blob broadcast + detection all-gather, no GPU, no timing)."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')}
+    out = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--plumbing',
+                          '--model', 'yolov7-tiny', '--batch', '3'], capture_output=True, text=True, env=env,
+                         timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, out.stdout
+    r = lines[0]
+    assert r['n_gpus'] == 2 and r['world_size_seen'] == 2 and r['all_ranks_ok'] and r['global_batch'] == 6

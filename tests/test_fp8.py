@@ -149,7 +149,7 @@ def test_gpu_fp8_map_parity(name):
           f'vs fp8 restatement {memu:.4f}; dets {[len(d) for d in pred]}')
     # e4m3 costs this random-weight network most of its detections (the restatement loses as much as the
     # kernels do); the GPU plan must be no worse than the restatement of its own arithmetic
-    assert m32 >= emu32 - 0.1
+    assert m32 >= emu32 - 0.02
 
 
 @pytest.mark.gpu

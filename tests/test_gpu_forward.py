@@ -101,11 +101,12 @@ def test_forward_fp16_layerwise_scale(name, B, H, W):
 def test_forward_fp16_map_parity(name):
     """fp16 plan judged like the reference's half() path (BASELINE metric: mAP@0.5 parity vs ref):
     mAP@0.5 of the GPU fp16 detections against the oracle's fp32 detections taken as ground truth
-    (both conf 0.25 / iou 0.45).  For scale, the oracle's own fp16-storage emulation of the
-    reference's half() path (oracle.yolo_ref.forward(half_storage=True)) is scored the same way."""
+    (both conf 0.25 / iou 0.45), on 8 frames.  The bar is the oracle's own fp16-storage emulation of
+    the reference's half() path (oracle.yolo_ref.forward(half_storage=True)) scored the same way,
+    minus 0.01: the fp16 plan is at least as faithful as the reference's half() path."""
     from oracle import metrics_ref, nms_ref, yolo_ref
     from utils.general import non_max_suppression
-    x = frames(2, 640, 640, seed=8)
+    x = frames(8, 640, 640, seed=8)
     net, fused = oracle_net(name)
     zr, _ = yolo_ref.forward(net, fused, x)
     z16e, _ = yolo_ref.forward(net, fused, x, half_storage=True)
@@ -120,4 +121,4 @@ def test_forward_fp16_map_parity(name):
     print(f'\n{name} fp16: mAP@0.5 {m50:.4f} (reference-half emulation {emu_map:.4f}), mAP@.5:.95 {m5095:.4f}; '
           f'z vs fp32 oracle: coord rel {((zc - zr.double()).abs() / sc)[..., :4].max():.3g}, '
           f'vs half emulation {((zc - z16e.double()).abs() / sc)[..., :4].max():.3g}')
-    assert m50 >= 0.95
+    assert m50 >= emu_map - 0.01 and m50 >= 0.95

@@ -115,6 +115,34 @@ def test_end_to_end_detections_match():
                 assert out_g[i][ig[r]][5].item() == out_r[i][k][5].item()
 
 
+@pytest.mark.parametrize('kw', [dict(conf_thres=0.25, iou_thres=0.45, topk=100),
+                                dict(conf_thres=0.5, iou_thres=0.3, topk=50),
+                                dict(conf_thres=0.05, iou_thres=0.6, topk=100)])
+def test_end2end_bitexact(kw):
+    """yv7_end2end (EfficientNMS_TRT contract, experimental.py:195-241) == the oracle's restatement of
+    the plugin (oracle/nms_ref.end2end), bit for bit: num_dets, boxes, scores, classes, padding."""
+    from oracle import nms_ref
+    from utils.general import end2end
+    z = _clustered_z(3, 6000, 80, seed=16)
+    z[1, :, 4] = 0.0                        # an image without candidates: num_dets 0, all padding
+    got = [t.cpu() for t in end2end(z.to(DEV), **kw)]
+    want = nms_ref.end2end(z, **kw)
+    for g_, w_, name in zip(got, want, ('num_dets', 'det_boxes', 'det_scores', 'det_classes')):
+        assert g_.dtype == w_.dtype and g_.shape == w_.shape, name
+        assert torch.equal(g_, w_), f'{name} differs'
+    assert int(want[0][1, 0]) == 0 and int(want[0][0, 0]) > 0
+
+
+def test_end2end_on_model_outputs():
+    from oracle import nms_ref, yolo_ref
+    from utils.general import end2end
+    net, fused = oracle_net('yolov7-tiny')
+    zr, _ = yolo_ref.forward(net, fused, frames(2, 640, 640, seed=9))
+    got = [t.cpu() for t in end2end(zr.to(DEV), 0.25, 0.45, 100)]
+    for g_, w_ in zip(got, nms_ref.end2end(zr, 0.25, 0.45, 100)):
+        assert torch.equal(g_, w_)
+
+
 def test_end2end_format():
     from utils.general import end2end
     z = _clustered_z(2, 3000, 80, seed=15)

@@ -1,0 +1,67 @@
+"""Every kernel configuration of the fp16 conv dispatch, forced onto every conv op of a real network
+(yv7_set_op_variant), checked op by op against a plain PyTorch fp32 reference of the same op on the
+op's own input (tests/opcheck.py).
+
+The tuned dispatch (csrc/conv_f16.hip launch_conv_f16 / choose) picks among these by tile count, so
+a small frame exercises only some of them; forcing each one on every layer shape of yolov7 /
+yolov7-tiny covers them all: the generic tile kernels (1, 2, 8), the 8-wave LDS-DMA rings (4-7),
+the halo and weight-stationary 3x3 kernels (10, 11, 15), every ring configuration with 1, 2 and 4 K
+splits (1CS: configuration C, S splits; the split-K hand-off of splitk_reduce), the persistent rings
+(201-206, BK 32: 211-217) and the two alternative Detect heads (92, 97).  A variant a layer's shape
+does not support falls back to the tuned kernel, which the check then covers again.
+Reference computation: models/common.py:110-111 (Conv.fuseforward), models/yolo.py:46-57 (Detect).
+"""
+import pytest
+import torch
+
+from helpers import fresh_model, frames
+from opcheck import check_ops, kernel_summary
+from yv7 import _lib as L
+
+pytestmark = pytest.mark.gpu
+DEV = 'cuda:0'
+
+CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15,
+                 100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
+                 201, 202, 203, 204, 205, 206, 211, 212, 213, 214, 215, 216, 217]
+DET_VARIANTS = [92, 97]
+
+
+@pytest.fixture(scope='module', autouse=True)
+def _no_miopen():
+    prev = torch.backends.cudnn.enabled
+    torch.backends.cudnn.enabled = False
+    yield
+    torch.backends.cudnn.enabled = prev
+
+
+@pytest.mark.parametrize('name,B,H,W', [('yolov7', 2, 256, 256), ('yolov7-tiny', 2, 192, 256)])
+def test_every_conv_variant(name, B, H, W):
+    m = fresh_model(name).to(DEV).half()
+    plan = m.plan()
+    x = frames(B, H, W, seed=31).to(DEV).half()
+    convs = [i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV]
+    dets = [i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_DETECT]
+    lines = []
+    for v in CONV_VARIANTS + DET_VARIANTS:
+        for i in (dets if v in DET_VARIANTS else convs):
+            plan.set_op_variant(i, v)
+        z, xs = plan.forward(x)
+        torch.cuda.synchronize()
+        out = check_ops(plan, x, B, H, W, raw=xs, z=z)
+        lines.append(f'variant {v}: ' + kernel_summary(out))
+        for i in (dets if v in DET_VARIANTS else convs):
+            plan.set_op_variant(i, 0)
+    print('\n' + '\n'.join(lines))
+
+
+def test_variant_api_rejects_hooks():
+    """Microbenchmark hooks (which skip work on purpose) cannot be forced through the ABI."""
+    m = fresh_model('yolov7-tiny').to(DEV).half()
+    plan = m.plan()
+    conv = next(i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV)
+    for v in (12, 13, 14, 16, 90, 91, 93, 94, 298, 160, 105):
+        with pytest.raises(RuntimeError):
+            plan.set_op_variant(conv, v)
+    with pytest.raises(RuntimeError):
+        plan.set_op_variant(len(plan.graph.ops) + 3, 0)

@@ -39,9 +39,16 @@ struct yv7_plan {
   void* weights = nullptr;
   size_t wbytes = 0;
   void* zero = nullptr;  // 4 KiB of zeros
-  // the workspaces (pointer, layout size) whose zero frames are known to be intact (see yv7_forward);
-  // several, so that sub-batches can run concurrently on their own streams and workspaces
-  std::vector<std::pair<const void*, size_t>> ws_ready;
+  // the workspaces whose zero frames are known to be intact for one layout (see yv7_forward); several,
+  // so that batches in flight can run concurrently on their own streams and workspaces
+  struct WsKey {
+    const void* ptr;
+    size_t bytes;
+    int B, H, W;
+  };
+  std::vector<WsKey> ws_ready;
+  // per-op kernel variant override (0 = tuned dispatch; yv7_set_op_variant)
+  std::vector<int> op_variant;
   // live profiling: events[f * (n_ops + 1) + i]
   std::vector<hipEvent_t> events;
   int prof_max = 0, prof_used = 0;
@@ -103,7 +110,8 @@ bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7
 
 // Geometry / operand fields of a CONV or DETECT op's kernel parameters (pointers into the workspace
 // are filled by the caller).
-yv7::ConvParams conv_params(const yv7_plan* p, const yv7_op_desc& o, int B, int H, int W) {
+yv7::ConvParams conv_params(const yv7_plan* p, size_t op, int B, int H, int W) {
+  const yv7_op_desc& o = p->ops[op];
   const auto& ti = p->tensors[o.src];
   const size_t es = elem_size(p->dtype);
   yv7::ConvParams c;
@@ -127,6 +135,7 @@ yv7::ConvParams conv_params(const yv7_plan* p, const yv7_op_desc& o, int B, int 
   c.M = B * c.Ho * c.Wo;
   c.xbytes = (uint32_t)tensor_bytes(p, ti, B, H, W);
   c.wbytes = (uint32_t)((size_t)((o.cout + 31) / 32 * 32) * c.kpad * es);
+  c.variant = p->op_variant[op];
   return c;
 }
 
@@ -143,9 +152,10 @@ struct SplitScratch {
 SplitScratch split_scratch(const yv7_plan* p, int B, int H, int W, size_t tensors_end) {
   SplitScratch s;
   if (p->dtype == YV7_DT_F16) {
-    for (const auto& o : p->ops) {
+    for (size_t i = 0; i < p->ops.size(); ++i) {
+      const auto& o = p->ops[i];
       if (o.kind == YV7_OP_CONV && !is_f8(o)) {
-        const yv7::ConvParams c = conv_params(p, o, B, H, W);
+        const yv7::ConvParams c = conv_params(p, i, B, H, W);
         s.part_bytes = std::max(s.part_bytes, yv7::conv_splitk_part_bytes(c));
         s.cnt_n = std::max(s.cnt_n, yv7::conv_splitk_tiles(c));
       } else if (is_f8(o)) {
@@ -242,6 +252,7 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
   p->dtype = d->dtype;
   p->tensors.assign(d->tensors, d->tensors + d->n_tensors);
   p->ops.assign(d->ops, d->ops + d->n_ops);
+  p->op_variant.assign(p->ops.size(), 0);
   p->nl = d->nl;
   p->na = d->na;
   p->no = d->no;
@@ -326,6 +337,41 @@ size_t yv7_workspace_bytes(const yv7_plan* p, int B, int H, int W) {
   return split_scratch(p, B, H, W, total).end;
 }
 
+int yv7_workspace_forget(yv7_plan* p, const void* ws, size_t bytes) {
+  if (!p || !ws) return fail(YV7_E_ARG, "yv7_workspace_forget: null argument");
+  const char* lo = reinterpret_cast<const char*>(ws);
+  const size_t n = bytes ? bytes : 1;
+  std::vector<yv7_plan::WsKey> keep;
+  for (const auto& w : p->ws_ready) {
+    const char* wl = reinterpret_cast<const char*>(w.ptr);
+    if (wl + w.bytes <= lo || lo + n <= wl) keep.push_back(w);
+  }
+  p->ws_ready = keep;
+  return 0;
+}
+
+// Kernel variants a caller may force per op: every real kernel configuration of the fp16 dispatch
+// (conv_f16.hip launch_conv_f16 / choose), never the microbenchmark hooks (90-99, 298; ws64's 12-14
+// and 16), which skip work on purpose.
+static bool variant_allowed(int kind, int v) {
+  if (v == 0) return true;
+  if (kind == YV7_OP_DETECT) return v == 92 || v == 97;
+  if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15) return true;
+  if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
+  return (v >= 201 && v <= 206) || (v >= 211 && v <= 217);
+}
+
+int yv7_set_op_variant(yv7_plan* p, int op, int variant) {
+  if (!p || op < 0 || op >= (int)p->ops.size()) return fail(YV7_E_ARG, "yv7_set_op_variant: bad op index");
+  const auto& o = p->ops[op];
+  if (o.kind != YV7_OP_CONV && o.kind != YV7_OP_DETECT)
+    return fail(YV7_E_ARG, "yv7_set_op_variant: op " + std::to_string(op) + " is not a CONV / DETECT op");
+  if (!variant_allowed(o.kind, variant))
+    return fail(YV7_E_ARG, "yv7_set_op_variant: variant " + std::to_string(variant) + " is not a kernel configuration");
+  p->op_variant[op] = variant;
+  return 0;
+}
+
 int64_t yv7_num_rows(const yv7_plan* p, int H, int W) {
   if (!p) return -1;
   int64_t n = 0;
@@ -367,21 +413,23 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   const unsigned char* wb = reinterpret_cast<const unsigned char*>(p->weights);
   hipError_t e = hipSuccess;
   // Kernels write only tensor interiors, so the zero frames survive from one forward to the next:
-  // the workspace is cleared when it is first seen (or its layout changes) and never again.
+  // a workspace is cleared the first time it is seen with this layout (pointer, size AND the batch
+  // geometry: (B, H, W) and (B, W, H) have equal sizes but different frames) and never again, until
+  // the caller hands the memory back with yv7_workspace_forget (include/yv7.h).
   {
     bool ready = false;
-    for (auto& w : p->ws_ready)
-      if (w.first == ws && w.second == total) ready = true;
+    for (const auto& w : p->ws_ready)
+      if (w.ptr == ws && w.bytes == total && w.B == B && w.H == H && w.W == W) ready = true;
     if (!ready) {
       if ((e = hipMemsetAsync(ws, 0, total, st)) != hipSuccess) return hip_fail(e, "hipMemsetAsync(workspace)");
       // a workspace overlapping this one (another layout of the same memory) is no longer intact
       const char* lo = reinterpret_cast<const char*>(ws);
-      std::vector<std::pair<const void*, size_t>> keep;
-      for (auto& w : p->ws_ready) {
-        const char* wl = reinterpret_cast<const char*>(w.first);
-        if (wl + w.second <= lo || lo + total <= wl) keep.push_back(w);
+      std::vector<yv7_plan::WsKey> keep;
+      for (const auto& w : p->ws_ready) {
+        const char* wl = reinterpret_cast<const char*>(w.ptr);
+        if (wl + w.bytes <= lo || lo + total <= wl) keep.push_back(w);
       }
-      keep.emplace_back(ws, total);
+      keep.push_back({ws, total, B, H, W});
       if (keep.size() > 8) keep.erase(keep.begin());
       p->ws_ready = keep;
     }
@@ -426,7 +474,7 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
       }
       case YV7_OP_CONV:
       case YV7_OP_DETECT: {
-        yv7::ConvParams c = conv_params(p, o, B, H, W);
+        yv7::ConvParams c = conv_params(p, i, B, H, W);
         c.x = wsb + off[o.src];
         c.w = wb + o.w_off;
         c.bias = reinterpret_cast<const float*>(wb + o.b_off);

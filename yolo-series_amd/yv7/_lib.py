@@ -56,6 +56,8 @@ SIGNATURES = {
     'yv7_plan_create': (_i, [ctypes.POINTER(NetDesc), _vp, _sz, _i, ctypes.POINTER(_vp)]),
     'yv7_plan_destroy': (None, [_vp]),
     'yv7_workspace_bytes': (_sz, [_vp, _i, _i, _i]),
+    'yv7_workspace_forget': (_i, [_vp, _vp, _sz]),
+    'yv7_set_op_variant': (_i, [_vp, _i, _i]),
     'yv7_num_rows': (_i64, [_vp, _i, _i]),
     'yv7_forward': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
     'yv7_profile_enable': (_i, [_vp, _i]),

@@ -27,16 +27,23 @@ def shard(global_batch: int, rank: int, world: int):
     return lo, lo + base + (1 if rank < rem else 0)
 
 
+def broadcast_blob(graph, device, group=None):
+    """Rank 0 packs `graph`'s weight blob, every rank receives it by one broadcast (RCCL over xGMI
+    on GPU ranks, gloo on CPU ranks); the other ranks never pack."""
+    if dist.get_rank(group) == 0:
+        blob = graph.weight_blob().to(device)
+    else:
+        blob = torch.empty(max(graph.nbytes, 1), dtype=torch.uint8, device=device)
+    dist.broadcast(blob, src=0, group=group)
+    return blob
+
+
 def broadcast_weights(model, device, dtype, group=None):
-    """Compile on every rank (cheap, host-only), pack on rank 0, RCCL-broadcast the packed blob."""
+    """Compile on every rank (cheap, host-only), pack on rank 0, RCCL-broadcast the packed blob and
+    create this rank's plan from it."""
     code = L.DT_F16 if dtype == torch.float16 else L.DT_F32
     g = compile_model(model, code)
-    if dist.get_rank(group) == 0:
-        blob = g.weight_blob().to(device)
-    else:
-        blob = torch.empty(max(g.nbytes, 1), dtype=torch.uint8, device=device)
-    dist.broadcast(blob, src=0, group=group)
-    return Plan(g, device, blob)
+    return Plan(g, device, broadcast_blob(g, device, group))
 
 
 def gather_detections(det, src_row, count, group=None):

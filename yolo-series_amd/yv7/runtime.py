@@ -69,6 +69,7 @@ class Plan:
                                         ctypes.byref(h)), 'yv7_plan_create')
         self._h = h
         self._ws = {}
+        self.variants = {}
         self.weight_bytes = weights.numel()
 
     @classmethod
@@ -116,6 +117,7 @@ class Plan:
         return cls(g, device, g.weight_blob().to(device))
 
     def __del__(self):
+        self._ws = {}
         h = getattr(self, '_h', None)
         if h is not None and h.value:
             try:
@@ -137,10 +139,25 @@ class Plan:
             if nbytes == 0:
                 L.check(-2, f'yv7_workspace_bytes(B={B}, H={H}, W={W})')
             for k in [k for k in self._ws if k[:3] != (B, H, W)]:   # keep one shape resident
-                del self._ws[k]
+                self._drop_workspace(k)
             ws = torch.empty(nbytes, dtype=torch.uint8, device=self.device)
             self._ws[key] = ws
         return ws
+
+    def _drop_workspace(self, key):
+        """Give a workspace back to the allocator.  libyv7 trusts the zero frame of a workspace it has
+        seen (include/yv7.h), so it is told first: the allocator may hand the same block back later,
+        after other tensors have written into it, and the next forward there must clear it again."""
+        ws = self._ws.pop(key)
+        L.check(L.lib().yv7_workspace_forget(self._h, ws.data_ptr(), ws.numel()), 'yv7_workspace_forget')
+
+    def set_op_variant(self, op, variant):
+        """Force op `op`'s kernel configuration (yv7_set_op_variant; 0 = tuned dispatch).  The split-K
+        scratch depends on it, so the cached workspaces are dropped."""
+        L.check(L.lib().yv7_set_op_variant(self._h, int(op), int(variant)), f'yv7_set_op_variant(op {op}, {variant})')
+        self.variants[int(op)] = int(variant)
+        for k in list(self._ws):
+            self._drop_workspace(k)
 
     def tensor_view(self, tensor_id, B, H, W):
         """NHWC view of an intermediate activation tensor of the last forward (debug / per-layer parity)."""
@@ -228,7 +245,9 @@ class Plan:
         return out
 
     def forward_into(self, x, z, raw=None, stream=None, rowbest=None, ws_slot=0):
-        """Forward into caller buffers; rowbest (optional): [B, N, 4] 32-bit yv7_row_best records."""
+        """Forward into caller buffers; rowbest (optional): [B, N, 4] 32-bit yv7_row_best records.
+        stream: a torch.cuda.Stream (default: the current stream); on a side stream every buffer the
+        forward touches is recorded on it, so the allocator cannot reuse it before the forward is done."""
         B, C, H, W = x.shape
         if C != 3:
             raise ValueError(f'expected a [B,3,H,W] image batch, got {tuple(x.shape)}')
@@ -237,12 +256,17 @@ class Plan:
         x = x.contiguous()
         ws = self.workspace(B, H, W, ws_slot)
         xdt = L.DT_F16 if x.dtype == torch.float16 else L.DT_F32
+        cur = torch.cuda.current_stream(self.device)
         if stream is None:
-            stream = torch.cuda.current_stream(self.device).cuda_stream
+            stream = cur
+        if stream != cur:
+            for t in (x, z, raw, rowbest, ws):
+                if t is not None:
+                    t.record_stream(stream)
         rc = L.lib().yv7_forward(self._h, x.data_ptr(), xdt, B, H, W, z.data_ptr(),
                                  raw.data_ptr() if raw is not None else None,
                                  rowbest.data_ptr() if rowbest is not None else None, ws.data_ptr(), ws.numel(),
-                                 stream)
+                                 stream.cuda_stream)
         L.check(rc, 'yv7_forward')
 
     def forward(self, x, want_raw=True):
@@ -283,6 +307,9 @@ class Inflight:
         run = Inflight(plan, B, H, W, streams=3)
         h = run.submit(x)                 # x [B,3,H,W] on the plan's device, produced on the current stream
         det, src_row, count = run.result(h)   # waits for that batch only; valid until S more submits
+
+    post(det, src_row, count) (optional) runs on the batch's stream after its NMS, e.g.
+    yv7.dist.gather_detections; whatever it returns is what result(h) hands back for that batch.
     """
 
     def __init__(self, plan, B, H, W, streams=3, conf_thres=0.25, iou_thres=0.45, max_det=300, post=None,
@@ -303,6 +330,7 @@ class Inflight:
         self.src = [torch.empty((B, max_det), dtype=torch.int64, device=dev) for _ in range(S)]
         self.cnt = [torch.empty((B,), dtype=torch.int32, device=dev) for _ in range(S)]
         self.done = [torch.cuda.Event() for _ in range(S)]
+        self.out = [None] * S   # post()'s result per slot
         self.n = 0
 
     def submit(self, x):
@@ -313,21 +341,34 @@ class Inflight:
         k = self.n % self.S
         s = self.streams[k]
         s.wait_stream(torch.cuda.current_stream(self.plan.device))   # x is ready
-        x.record_stream(s)
-        self.plan.forward_into(x, self.z[k], rowbest=self.rowbest[k], stream=s.cuda_stream, ws_slot=k)
+        self.plan.forward_into(x, self.z[k], rowbest=self.rowbest[k], stream=s, ws_slot=k)
         with torch.cuda.stream(s):
             nms_batched(self.z[k], self.conf, self.iou, max_det=self.max_det,
                         out=(self.det[k], self.src[k], self.cnt[k]), rowbest=self.rowbest[k])
+            out = (self.det[k], self.src[k], self.cnt[k])
             if self.post is not None:
-                self.post(self.det[k], self.src[k], self.cnt[k])
+                out = self.post(*out)
+        self.out[k] = out
         self.done[k].record(s)
         self.n += 1
         return self.n - 1
 
     def result(self, h):
-        """(det [B,max_det,6], src_row [B,max_det], count [B]) of submission h, once it has finished."""
+        """(det [B,max_det,6], src_row [B,max_det], count [B]) of submission h once it has finished, or
+        what post() returned for it."""
         if not (self.n - self.S <= h < self.n):
             raise IndexError(f'batch {h} is no longer buffered (last {self.S} of {self.n} submissions)')
         k = h % self.S
         self.done[k].synchronize()
-        return self.det[k], self.src[k], self.cnt[k]
+        return self.out[k]
+
+    def close(self):
+        """Wait for every batch in flight (their buffers and workspaces are then free to go)."""
+        for s in self.streams:
+            s.synchronize()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
