@@ -1011,6 +1011,199 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// s_waitcnt immediate (gfx9 family encoding): vmcnt(vm) expcnt(none) lgkmcnt(0)
+constexpr int waitcnt_vm_lgkm0(int vm) { return (vm & 15) | (7 << 4) | (((vm >> 4) & 3) << 14); }
+
+// ---------------------------------------------------------------------------------------------
+// Pipelined persistent ring.  The persistent ring above reads both 32-deep fragment sets of a K step
+// right after its barrier and only then issues the MFMAs, and its barrier puts the two waves of a
+// SIMD in phase every step: both read, the matrix pipe idles, both multiply.  Here each wave keeps
+// two fragment register sets and the step is split around the barrier:
+//     reads F1(k)            (LDS stage k, 2nd 32-deep half)  |  MFMA F0(k)
+//     lgkmcnt(0) + vmcnt(stage k+1 landed) + s_barrier
+//     DMA stage k+2 into stage k's slot (every wave is done reading stage k)
+//     reads F0(k+1)          (stage k+1, 1st half)            |  MFMA F1(k) [+ tile epilogue]
+// so every fragment read is in flight under the wave's own previous MFMA cluster.  Two LDS stages of
+// BK = 64; a stage's DMA has one K step of MFMAs to land (as in the ring above).  The tile walk, the
+// DMA addressing and the register epilogue are the persistent ring's.
+template <int BM, int BN, int WM, int WN, bool ONE, int ACT>
+__global__ __launch_bounds__(64 * WM * WN, (2 * (BM + BN) * 128 <= 76 * 1024) ? 2 : 1) void conv_f16_pp_kernel(
+    const ConvParams p) {
+  constexpr int BK = 64, STAGES = 2;
+  constexpr int NW = WM * WN, NTH = 64 * NW;
+  constexpr int WTM = BM / WM, WTN = BN / WN;
+  constexpr int TM = WTM / 16, TN = WTN / 16;
+  constexpr int RB_ = BK * 2;              // LDS bytes per tile row
+  constexpr int RPI = 8;                   // tile rows per DMA wave-instruction (1 KiB)
+  constexpr int RA = BM / RPI / NW, RB = BN / RPI / NW;
+  static_assert(RA * RPI * NW == BM && RB * RPI * NW == BN, "tile rows must split into DMA groups per wave");
+  static_assert(TN % 2 == 0, "the epilogue pairs 16-channel groups");
+  constexpr int NST = TM * TN / 2;         // epilogue stores per lane per tile
+  constexpr int STAGE = (BM + BN) * RB_;
+  constexpr int BIAS = 4096;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + BIAS];
+  float* bias_l = reinterpret_cast<float*>(smem + STAGES * STAGE);
+
+  const int tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, li = lane & 15;
+  const int lr = lane >> 3;
+  const int c = swz_bk<BK>(lr, lane & 7);
+
+  const int nN = (p.cout + BN - 1) / BN;
+  const int T = ((p.M + BM - 1) / BM) * nN;
+  const int G = gridDim.x;
+  const int nk = p.kpad / BK;
+  const int ntl = (T - (int)blockIdx.x + G - 1) / G;
+  const int nsteps = ntl * nk;
+
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto wr = make_rsrc(p.w, p.wbytes);
+  const auto yr = make_rsrc(p.y, 0x7fffffffu);
+
+  for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
+
+  AWalk<ONE, RA, BK> aw;
+  uint32_t b_off0 = 0;   // weight row of group j: b_off0 + j * bstride (one VGPR instead of RB)
+  const uint32_t bstride = (uint32_t)(NW * RPI * p.kpad * 2);
+  int ig = 0, it = 0, ikt = 0;
+  auto issue_next = [&]() {
+    if (ikt == 0) {
+      const int t = blockIdx.x + it * G;
+      const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+      aw.init(p, c, 0);
+      PixelWalk pw(p, m0 + wave * RPI + lr);
+#pragma unroll
+      for (int j = 0; j < RA; ++j) {
+        if (j) pw.advance(p, NW * RPI);
+        aw.off[j] = a_origin(p, pw.b, pw.ho, pw.wo, c);
+      }
+      b_off0 = (uint32_t)(((n0 + wave * RPI + lr) * p.kpad + c * 8) * 2);
+    }
+    unsigned char* As = smem + (ig & 1) * STAGE;
+    unsigned char* Bs = As + BM * RB_;
+    aw.step(p, ikt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * RPI * RB_, vo, so); });
+#pragma unroll
+    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * RPI * RB_, b_off0 + j * bstride, (uint32_t)ikt * BK * 2);
+    ++ig;
+    if (++ikt == nk) { ikt = 0; ++it; }
+  };
+
+  f4 acc[TN][TM];
+  int cm0 = 0, cn0 = 0;
+  auto init_tile = [&](int i) {
+    const int t = blockIdx.x + i * G;
+    cm0 = (t / nN) * BM;
+    cn0 = (t % nN) * BN;
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int col = cn0 + wn * WTN + j * 16 + g * 4;
+      f4 bv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? bias_l[col + e] : 0.0f;
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) acc[j][ii] = bv;
+    }
+  };
+  const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
+  auto epilogue = [&]() {
+    PixelWalk pw(p, cm0 + wm * WTM + li);
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii) {
+      if (ii) pw.advance(p, 16);
+      const int m = cm0 + wm * WTM + ii * 16 + li;
+      const uint32_t yo = (uint32_t)((pix_index(pw.b, pw.ho, pw.wo, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
+#pragma unroll
+      for (int mp = 0; mp < TN / 2; ++mp) {
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+        h4 va, vb;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          va[e] = (_Float16)act_t<ACT>(acc[2 * mp][ii][e]);
+          vb[e] = (_Float16)act_t<ACT>(acc[2 * mp + 1][ii][e]);
+        }
+        const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
+        const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+        const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+        const u4 v = {s0[0], s1[0], s0[1], s1[1]};
+        const int n = cn0 + wn * WTN + mp * 32 + (int)lane_ch;
+        const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
+        __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+      }
+    }
+  };
+
+  // fragment sets: F0 = K elements [0, 32) of a stage, F1 = [32, 64)
+  u4 xa0[TM], wb0[TN], xa1[TM], wb1[TN];
+  auto read_frag = [&](int slot, int sb, u4 (&xa)[TM], u4 (&wb)[TN]) {
+    const unsigned char* As = smem + slot * STAGE;
+    const unsigned char* Bs = As + BM * RB_;
+    const int ch = sb * 4 + g;
+#pragma unroll
+    for (int ii = 0; ii < TM; ++ii) {
+      const int row = wm * WTM + ii * 16 + li;
+      xa[ii] = *reinterpret_cast<const u4*>(As + row * RB_ + swz_bk<BK>(row, ch) * 16);
+    }
+#pragma unroll
+    for (int j = 0; j < TN; ++j) {
+      const int row = wn * WTN + j * 16 + li;
+      wb[j] = *reinterpret_cast<const u4*>(Bs + row * RB_ + swz_bk<BK>(row, ch) * 16);
+    }
+  };
+  auto mfma = [&](const u4 (&xa)[TM], const u4 (&wb)[TN]) {
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii)
+        acc[j][ii] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]), __builtin_bit_cast(h8, xa[ii]),
+                                                            acc[j][ii], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+  };
+
+  issue_next();
+  if (nsteps > 1) issue_next();
+  if (nsteps > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(RA + RB) : "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  init_tile(0);
+  read_frag(0, 0, xa0, wb0);
+
+  int ci = 0, ckt = 0;
+  bool stores_pending = false;   // the previous step ended a tile: its NST stores are younger than stage gs+1
+  for (int gs = 0; gs < nsteps; ++gs) {
+    const int slot = gs & 1;
+    read_frag(slot, 1, xa1, wb1);
+    mfma(xa0, wb0);
+    __builtin_amdgcn_sched_barrier(0);
+    // F1(gs) reads done (so the whole stage gs has been read by this wave) and stage gs+1 landed.
+    // The builtin (not inline asm), on every path, lets the compiler's own wait insertion see that the
+    // F1 reads are retired, so it does not hold F1's MFMAs back for the F0(gs+1) reads issued below.
+    if (stores_pending) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(NST));
+    else __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
+    if (gs + 1 < nsteps) {
+      __builtin_amdgcn_s_barrier();
+      __builtin_amdgcn_sched_barrier(0);
+      if (ig < nsteps) issue_next();   // stage gs+2 -> slot gs & 1
+    }
+    // F0(gs+1) (after the last step a harmless read of the other slot): issued on every path, so the
+    // compiler's wait insertion (which does not credit the wait above) sees the same read sequence
+    // ahead of F1's MFMAs on every path and counts only the F0 reads as younger
+    read_frag(slot ^ 1, 0, xa0, wb0);
+    mfma(xa1, wb1);
+    stores_pending = false;
+    if (++ckt == nk) {
+      epilogue();
+      stores_pending = true;
+      ckt = 0;
+      if (++ci < ntl) init_tile(ci);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int BK>
 hipError_t launch_pring_act(const ConvParams& p, int grid, hipStream_t st) {
   if (p.act == 1)
@@ -1031,6 +1224,21 @@ int device_cus() {
     return v;
   }();
   return n;
+}
+
+template <int BM, int BN, int WM, int WN, bool ONE>
+hipError_t launch_pp(const ConvParams& p, int occ, hipStream_t st) {
+  if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8) return hipErrorInvalidValue;
+  const long T = (long)((p.M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
+  const long cap = (long)device_cus() * occ;
+  const int grid = (int)(T < cap ? T : cap);
+  if (p.act == 1)
+    hipLaunchKernelGGL((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 1>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  else if (p.act == 2)
+    hipLaunchKernelGGL((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 2>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  else
+    hipLaunchKernelGGL((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 0>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  return hipGetLastError();
 }
 
 // occ: resident blocks per CU the grid is sized for
@@ -1220,6 +1428,10 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 215) return launch_pring<256, 128, 2, 2, 3, 32>(p, one, 2, st);
     if (variant == 216) return launch_pring<128, 256, 2, 2, 3, 32>(p, one, 2, st);
     if (variant == 217) return launch_pring<128, 128, 2, 2, 2, 64>(p, one, 2, st);
+    // pipelined persistent rings (conv_f16_pp_kernel)
+    if (variant == 221) return one ? launch_pp<256, 256, 2, 4, true>(p, 1, st) : launch_pp<256, 256, 2, 4, false>(p, 1, st);
+    if (variant == 222) return one ? launch_pp<128, 128, 2, 2, true>(p, 2, st) : launch_pp<128, 128, 2, 2, false>(p, 2, st);
+    if (variant == 223) return one ? launch_pp<256, 128, 4, 2, true>(p, 1, st) : launch_pp<256, 128, 4, 2, false>(p, 1, st);
   }
   if (!det && p.cout > 32) {
     // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/

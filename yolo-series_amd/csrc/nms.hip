@@ -16,6 +16,9 @@
 //                  sorted candidates the workgroup builds the 64 x 64 "i suppresses j" bitmask, one
 //                  wave resolves it with bit operations, the workgroup then strikes later candidates that
 //                  a box kept in that block overlaps (IoU > thr); stops at max_det kept (:705-706).
+// The single-label call without a class filter (detect.py's defaults, the serving path) takes a
+// two-launch fast path instead (nms_compact + nms_fast below: sort keys compacted by atomics, then
+// sort and a lazy greedy scan per image that stops once max_det boxes are kept).
 // IoU arithmetic is torchvision's: area=(x2-x1)*(y2-y1), inter=max(0,.)*max(0,.),
 // inter / (area_i + area_j - inter) > thr, all fp32; this file is built with -ffp-contract=off.
 #include <hip/hip_runtime.h>
@@ -484,14 +487,223 @@ __global__ __launch_bounds__(SORT_T) void nms_greedy(const NmsArgs a) {
   if (threadIdx.x == 0) a.count[b] = total < a.max_det ? total : a.max_det;
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fast path: single-label, no class filter (detect.py's and the bench's call, general.py:683-684).
+// Two launches instead of five:
+//   nms_compact  a lane per row from the yv7_row_best records: rows with obj > conf and best
+//                obj*cls > conf append one 64-bit key ((~conf bits) << 32 | row) to their image's list
+//                (wave-aggregated atomic slot; list order is arbitrary — the key carries the
+//                reference's tie order, the row index, so sorting restores it exactly)
+//   nms_fast     one workgroup per image: bitonic sort of the keys in LDS, then a LAZY greedy scan in
+//                sorted order, 64 candidates at a time: each candidate is tested against every box
+//                already kept (IoU > thr, class-offset boxes) and against the earlier members of its
+//                block (64 x 64 mask, resolved by one wave with bit operations).  A candidate survives
+//                iff no earlier KEPT box overlaps it — exactly torchvision's greedy definition — so the
+//                scan touches only the sorted prefix that reaches max_det (for typical frames about
+//                max_det candidates), never the whole list.
+struct FastArgs {
+  const float* z;
+  const RowBest* rb;
+  int B, N, no;
+  float conf, iou;
+  int agnostic, max_det, max_nms;
+  size_t kcap;        // per-image key capacity (pow2 >= N)
+  uint64_t* keys;     // [B][kcap]
+  int* ncand;         // [B]
+  float* det;
+  int64_t* src_row;
+  int32_t* count;
+};
+
+constexpr int FAST_MAX_DET = 1024;   // kept-box list in LDS
+
+__global__ __launch_bounds__(NT) void nms_compact(const FastArgs a) {
+  const int b = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const RowBest* rb = a.rb + (size_t)b * a.N;
+  uint64_t* keys = a.keys + (size_t)b * a.kcap;
+  for (int r0 = blockIdx.x * NT + (threadIdx.x & ~63); r0 < a.N; r0 += gridDim.x * NT) {
+    const int row = r0 + lane;
+    bool c = false;
+    float conf = 0.f;
+    if (row < a.N) {
+      const RowBest r = rb[row];
+      c = r.obj > a.conf && r.conf > a.conf;   // :637 / :653 then :684
+      conf = r.conf;
+    }
+    const uint64_t m = __ballot(c);
+    if (!m) continue;
+    int base = 0;
+    if (lane == 0) base = atomicAdd(a.ncand + b, __popcll(m));
+    base = __shfl(base, 0);
+    if (c) {
+      const int k = base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+      keys[k] = ((uint64_t)(~__float_as_uint(conf)) << 32) | (uint32_t)row;
+    }
+  }
+}
+
+__global__ __launch_bounds__(SORT_T) void nms_fast(const FastArgs a) {
+  const int b = blockIdx.x;
+  const int n = min(a.ncand[b], a.N);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  constexpr int NW = SORT_T / 64;
+  extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
+  uint64_t* skeys = reinterpret_cast<uint64_t*>(fsm);                              // [LDS_SORT_MAX]
+  float4* kbox = reinterpret_cast<float4*>(fsm + LDS_SORT_MAX * 8);                 // kept boxes (offset)
+  float* karea = reinterpret_cast<float*>(kbox + FAST_MAX_DET);
+  __shared__ float4 bbox[64], braw[64];
+  __shared__ float barea[64], bconf[64];
+  __shared__ int bcls[64], brow[64];
+  __shared__ uint64_t sup[64];
+  __shared__ unsigned char pre[64];
+  __shared__ int total_s;
+
+  // ---- sort: keys ascending = (conf descending, row ascending), torchvision's stable order
+  int P = 1;
+  while (P < n) P <<= 1;
+  uint64_t* keys = a.keys + (size_t)b * a.kcap;
+  const bool in_lds = P <= LDS_SORT_MAX;
+  uint64_t* s = in_lds ? skeys : keys;
+  if (in_lds) {
+    for (int i = tid; i < P; i += SORT_T) skeys[i] = i < n ? keys[i] : ~0ull;
+  } else {
+    for (int i = n + tid; i < P; i += SORT_T) keys[i] = ~0ull;   // kcap >= P (pow2 >= N >= n)
+  }
+  __syncthreads();
+  if (in_lds) {
+    for (int k = 2; k <= P; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < P; i += SORT_T) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const uint64_t ki = skeys[i], kj = skeys[ixj];
+            if ((ki > kj) == ((i & k) == 0)) { skeys[i] = kj; skeys[ixj] = ki; }
+          }
+        }
+        __syncthreads();
+      }
+  } else {
+    for (int k = 2; k <= P; k <<= 1)
+      for (int j = k >> 1; j > 0; j >>= 1) {
+        for (int i = tid; i < P; i += SORT_T) {
+          const int ixj = i ^ j;
+          if (ixj > i) {
+            const uint64_t ki = keys[i], kj = keys[ixj];
+            if ((ki > kj) == ((i & k) == 0)) { keys[i] = kj; keys[ixj] = ki; }
+          }
+        }
+        __syncthreads();   // (global keys: one workgroup, its own L1/L2 view; the fence orders them)
+      }
+  }
+  const int m = n < a.max_nms ? n : a.max_nms;   // :698-699 (first max_nms in sorted order)
+  if (tid == 0) total_s = 0;
+  __syncthreads();
+  const float* zb = a.z + (size_t)b * a.N * a.no;
+  const RowBest* rb = a.rb + (size_t)b * a.N;
+  for (int base = 0; base < m; base += 64) {
+    // (1) the block's 64 candidates: boxes from z (xywh2xyxy, general.py:275-282), class from the row
+    //     record, class offset (general.py:702-703) unless agnostic
+    if (tid < 64) {
+      const int j = base + tid;
+      if (j < m) {
+        const uint64_t key = s[j];
+        const int row = (int)(uint32_t)key;
+        const float conf = __uint_as_float(~(uint32_t)(key >> 32));
+        const float* zr = zb + (size_t)row * a.no;
+        const float cx = zr[0], cy = zr[1], w = zr[2], h = zr[3];
+        float4 r;
+        r.x = cx - w / 2.0f;
+        r.y = cy - h / 2.0f;
+        r.z = cx + w / 2.0f;
+        r.w = cy + h / 2.0f;
+        const int cls = rb[row].cls;
+        const float off = a.agnostic ? 0.0f : (float)cls * (float)MAX_WH;
+        float4 bx;
+        bx.x = r.x + off;
+        bx.y = r.y + off;
+        bx.z = r.z + off;
+        bx.w = r.w + off;
+        braw[tid] = r;
+        bbox[tid] = bx;
+        barea[tid] = (bx.z - bx.x) * (bx.w - bx.y);
+        bconf[tid] = conf;
+        bcls[tid] = cls;
+        brow[tid] = row;
+      }
+    }
+    __syncthreads();
+    const int total = total_s;
+    // (2) each wave: its 4 block rows i against the later block members (lanes) -> sup[i]; and its 4
+    //     candidates against every kept box so far -> pre[i] (suppressed by an earlier kept box)
+#pragma unroll
+    for (int q = 0; q < 64 / NW; ++q) {
+      const int i = wv * (64 / NW) + q;
+      const int ig = base + i;
+      const int jg = base + lane;
+      bool hit = false;
+      if (ig < m && jg < m && lane > i) hit = iou_gt(bbox[i], barea[i], bbox[lane], barea[lane], a.iou);
+      const uint64_t msk = __ballot(hit);
+      bool kh = false;
+      if (ig < m) {
+        const float4 bi = bbox[i];
+        const float ai = barea[i];
+        for (int t = lane; t < total && !kh; t += 64) kh = iou_gt(kbox[t], karea[t], bi, ai, a.iou);
+      }
+      const bool anyk = __ballot(kh) != 0ull;
+      if (lane == 0) {
+        sup[i] = msk;
+        pre[i] = anyk ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    // (3) wave 0 resolves the block in order
+    if (tid < 64) {
+      const int j = base + lane;
+      const bool valid = j < m && !pre[lane];
+      const uint64_t my_sup = sup[lane];
+      uint64_t alive = __ballot(valid);
+      uint64_t kept = 0;
+      while (alive) {
+        const int i = __ffsll((long long)alive) - 1;
+        kept |= 1ull << i;
+        alive &= ~__shfl(my_sup, i) & ~(1ull << i);
+      }
+      const int nk = __popcll(kept);
+      if ((kept >> lane) & 1ull) {
+        const int di = total + __popcll(kept & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+        if (di < a.max_det) {
+          kbox[di] = bbox[lane];
+          karea[di] = barea[lane];
+          const float4 r = braw[lane];
+          float* d = a.det + ((size_t)b * a.max_det + di) * 6;
+          d[0] = r.x;
+          d[1] = r.y;
+          d[2] = r.z;
+          d[3] = r.w;
+          d[4] = bconf[lane];
+          d[5] = (float)bcls[lane];
+          a.src_row[(size_t)b * a.max_det + di] = brow[lane];
+        }
+      }
+      if (lane == 0) total_s = total + nk;
+    }
+    __syncthreads();
+    if (total_s >= a.max_det) break;   // :705-706
+  }
+  if (tid == 0) a.count[b] = total_s < a.max_det ? total_s : a.max_det;
+}
+
 struct Layout {
   size_t cnt, offs, bconf, bcls, ncand, cand, keys, order, sbox, sarea, total;
   size_t cap, pcap;
+  size_t fkeys, frb, kcap;   // fast path: [B][kcap] sort keys, [B][N] row records (when computed here)
 };
 
 inline size_t al(size_t x) { return (x + 255) & ~(size_t)255; }
 
 Layout layout(int B, int N, int nc, int multi, int max_nms) {
+  multi = multi && nc > 1;   // multi_label &= nc > 1 (general.py:646): the layout follows the path taken
   Layout L;
   L.cap = (size_t)N * (multi ? (size_t)nc : 1);
   L.pcap = 1;
@@ -507,6 +719,10 @@ Layout layout(int B, int N, int nc, int multi, int max_nms) {
   L.order = o; o = al(o + sizeof(int) * (size_t)B * max_nms);
   L.sbox = o; o = al(o + sizeof(float4) * (size_t)B * max_nms);
   L.sarea = o; o = al(o + sizeof(float) * (size_t)B * max_nms);
+  L.kcap = 1;
+  while (L.kcap < (size_t)N) L.kcap <<= 1;
+  L.fkeys = o; o = al(o + (multi ? 0 : sizeof(uint64_t) * (size_t)B * L.kcap));
+  L.frb = o; o = al(o + (multi ? 0 : sizeof(RowBest) * (size_t)B * N));
   L.total = o;
   return L;
 }
@@ -591,6 +807,47 @@ hipError_t launch_nms(const float* z, const void* rowbest, int B, int N, int no,
   if ((e = hipMemsetAsync(src_row, 0xff, sizeof(int64_t) * (size_t)B * max_det, st)) != hipSuccess) return e;
   int gx = (N + NT - 1) / NT;   // a lane per row
   if (gx > 1024) gx = 1024;
+  if (!a.multi && !classes && !per_class && max_det <= FAST_MAX_DET) {
+    // fast path (single label, no class filter): compact -> sort + lazy greedy
+    FastArgs f;
+    f.z = z;
+    f.rb = reinterpret_cast<const RowBest*>(rowbest);
+    if (!rowbest) {   // derive the row records from z first (plans whose head does not write them)
+      RowBest* rb = reinterpret_cast<RowBest*>(w + L.frb);
+      int gr = (N + 31) / 32;
+      if (gr > 1024) gr = 1024;
+      hipLaunchKernelGGL(row_best_kernel, dim3(gr, B), dim3(NT), 0, st, z, N, no, rb);
+      if ((e = hipGetLastError()) != hipSuccess) return e;
+      f.rb = rb;
+    }
+    f.B = B;
+    f.N = N;
+    f.no = no;
+    f.conf = conf;
+    f.iou = iou;
+    f.agnostic = agnostic;
+    f.max_det = max_det;
+    f.max_nms = max_nms;
+    f.kcap = L.kcap;
+    f.keys = reinterpret_cast<uint64_t*>(w + L.fkeys);
+    f.ncand = a.ncand;
+    f.det = det;
+    f.src_row = src_row;
+    f.count = count;
+    if ((e = hipMemsetAsync(a.ncand, 0, sizeof(int) * (size_t)B, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(nms_compact, dim3(gx, B), dim3(NT), 0, st, f);
+    if ((e = hipGetLastError()) != hipSuccess) return e;
+    const size_t lds = sizeof(uint64_t) * LDS_SORT_MAX + (sizeof(float4) + sizeof(float)) * FAST_MAX_DET;
+    static bool fast_attr = false;
+    if (!fast_attr) {
+      if ((e = hipFuncSetAttribute((const void*)nms_fast, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) !=
+          hipSuccess)
+        return e;
+      fast_attr = true;
+    }
+    hipLaunchKernelGGL(nms_fast, dim3(B), dim3(SORT_T), lds, st, f);
+    return hipGetLastError();
+  }
   if (rowbest && !a.multi && !classes)
     hipLaunchKernelGGL(nms_rows_from_best, dim3(gx, B), dim3(NT), 0, st, a, reinterpret_cast<const RowBest*>(rowbest));
   else

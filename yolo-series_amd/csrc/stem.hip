@@ -16,6 +16,8 @@
 //   3. conv B on the MFMA: M = TBY*TBX, N = CB, K = 9 taps x CA; each wave owns 16 output channels and
 //      holds their 9 taps of weight fragments in registers (loaded at entry, under the patch load)
 //   4. + bias + act -> LDS tile -> 16-byte NHWC stores into the destination channel slice.
+#include <cstdlib>
+
 #include "yv7_kernels.h"
 
 namespace yv7 {
@@ -48,12 +50,15 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   const int HA = p.H / SA, WA = p.W / SA;          // conv-A output size
   const int HB = HA / 2, WB = WA / 2;              // conv-B output size
   const int tiles_x = (WB + TBX - 1) / TBX, tiles_y = (HB + TBY - 1) / TBY;
-  int t = blockIdx.x;
-  const int b = t / (tiles_x * tiles_y);
-  t -= b * tiles_x * tiles_y;
-  const int oy0 = (t / tiles_x) * TBY, ox0 = (t % tiles_x) * TBX;
-  const int ay0 = 2 * oy0 - 1, ax0 = 2 * ox0 - 1;
-  const int iy0 = SA * ay0 - 1, ix0 = SA * ax0 - 1;
+  const int ntiles = p.B * tiles_x * tiles_y;
+  // persistent: this block's tiles are blockIdx.x, + gridDim.x, ...; tile geometry
+  int b = 0, oy0 = 0, ox0 = 0, ay0 = 0, ax0 = 0;
+  auto tile_geom = [&](int t, int& tb, int& ty, int& tx) {
+    tb = t / (tiles_x * tiles_y);
+    t -= tb * tiles_x * tiles_y;
+    ty = (t / tiles_x) * TBY;
+    tx = (t % tiles_x) * TBX;
+  };
 
   // conv-B weight fragments of this wave's 16 output channels, all 9 taps (K = 32 per tap = CA)
   u4 wfr[9];
@@ -62,21 +67,40 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
     wfr[tap] = *reinterpret_cast<const u4*>(reinterpret_cast<const _Float16*>(p.wb) +
                                             (size_t)(wave * 16 + li) * p.kpad_b + tap * CA + g * 8);
 
-  // 1. image patch -> LDS (fp16, channel 3 zero)
-  const S* xb = reinterpret_cast<const S*>(p.x) + (size_t)b * 3 * p.H * p.W;
-  for (int i = tid; i < PY * PX; i += NT) {
-    const int py = i / PX, px = i - py * PX;
-    const int iy = iy0 + py, ix = ix0 + px;
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    h4 v = {(_Float16)0.f, (_Float16)0.f, (_Float16)0.f, (_Float16)0.f};
-    if ((unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2) {
-      const size_t o = (size_t)iy * p.W + ix;
-      v[0] = (_Float16)(float)xb[o];
-      v[1] = (_Float16)(float)xb[o + (size_t)p.H * p.W];
-      v[2] = (_Float16)(float)xb[o + 2 * (size_t)p.H * p.W];
+  // 1. image patch (PY x PX x 3, zero outside the image): the NEXT tile's pixels are loaded into
+  //    registers while the current tile computes, and written to LDS (fp16, channel 3 zero) at the
+  //    top of the next iteration, so the image loads' latency sits under conv A / conv B.
+  constexpr int PPT = (PY * PX + NT - 1) / NT;   // patch pixels per thread
+  S pre[PPT][3];
+  auto prefetch = [&](int t) {
+    int tb, ty, tx;
+    tile_geom(t, tb, ty, tx);
+    const int iy0 = SA * (2 * ty - 1) - 1, ix0 = SA * (2 * tx - 1) - 1;
+    const S* xb = reinterpret_cast<const S*>(p.x) + (size_t)tb * 3 * p.H * p.W;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int i = tid + k * NT;
+      const int py = i / PX, px = i - py * PX;
+      const int iy = iy0 + py, ix = ix0 + px;
+      pre[k][0] = pre[k][1] = pre[k][2] = (S)0.f;
+      if (i < PY * PX && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2) {
+        const size_t o = (size_t)iy * p.W + ix;
+        pre[k][0] = xb[o];
+        pre[k][1] = xb[o + (size_t)p.H * p.W];
+        pre[k][2] = xb[o + 2 * (size_t)p.H * p.W];
+      }
     }
-    *reinterpret_cast<h4*>(patch + i * 4) = v;
-  }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int i = tid + k * NT;
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      const h4 v = {(_Float16)(float)pre[k][0], (_Float16)(float)pre[k][1], (_Float16)(float)pre[k][2],
+                    (_Float16)0.f};
+      if (i < PY * PX) *reinterpret_cast<h4*>(patch + i * 4) = v;
+    }
+  };
   // conv A's K layout on the MFMA: 4 halves per tap (3 channels + the patch's zero 4th channel),
   // two taps per 8-half lane group, so a lane's A fragment is two 8-byte patch pixels — for the
   // horizontally adjacent pairs one contiguous 16 bytes — instead of eight scattered halves.
@@ -126,6 +150,13 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   for (int nt = 0; nt < NAT; ++nt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) ba_l[nt][e] = p.ba[nt * 16 + g * 4 + e] * sa_scale;
+  if ((int)blockIdx.x < ntiles) prefetch(blockIdx.x);
+  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  tile_geom(tile, b, oy0, ox0);
+  ay0 = 2 * oy0 - 1;
+  ax0 = 2 * ox0 - 1;
+  commit();
+  if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);
   __syncthreads();
 
   // 2. conv A on MFMA -> abuf
@@ -226,13 +257,24 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
       *reinterpret_cast<u4*>(y + pix_index(b, oy, ox, HB, WB) * p.yc + p.yoff + ch * 8) =
           *reinterpret_cast<const u4*>(smem + mb * CPITCH + ch * 16);
   }
+  __syncthreads();   // the output staging overlaps the next tile's patch
+  }
 }
 
 template <typename S, int CA, int CB, int SA, int ACT_A, int ACT_B>
 hipError_t stem_t(const StemParams& p, hipStream_t st) {
   constexpr int TBY = 8, TBX = 16;
   const int HB = p.H / SA / 2, WB = p.W / SA / 2;
-  const int nblk = p.B * ((HB + TBY - 1) / TBY) * ((WB + TBX - 1) / TBX);
+  const int ntiles = p.B * ((HB + TBY - 1) / TBY) * ((WB + TBX - 1) / TBX);
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  static const int occ = [] { const char* e = getenv("YV7_STEM_OCC"); return e ? atoi(e) : 2; }();
+  const int nblk = ntiles < cus * occ ? ntiles : cus * occ;   // persistent: blocks walk the tiles
   hipLaunchKernelGGL((stem_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B>), dim3(nblk), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
