@@ -17,8 +17,8 @@
 //                  wave resolves it with bit operations, the workgroup then strikes later candidates that
 //                  a box kept in that block overlaps (IoU > thr); stops at max_det kept (:705-706).
 // The single-label call without a class filter (detect.py's defaults, the serving path) takes a
-// two-launch fast path instead (nms_compact + nms_fast below: sort keys compacted by atomics, then
-// sort and a lazy greedy scan per image that stops once max_det boxes are kept).
+// one-launch fast path instead (nms_fast below: compaction, register bitonic sort and a lazy greedy
+// scan per image that stops once max_det boxes are kept).
 // IoU arithmetic is torchvision's: area=(x2-x1)*(y2-y1), inter=max(0,.)*max(0,.),
 // inter / (area_i + area_j - inter) > thr, all fp32; this file is built with -ffp-contract=off.
 #include <hip/hip_runtime.h>
@@ -489,136 +489,208 @@ __global__ __launch_bounds__(SORT_T) void nms_greedy(const NmsArgs a) {
 
 // ---------------------------------------------------------------------------------------------
 // Fast path: single-label, no class filter (detect.py's and the bench's call, general.py:683-684).
-// Two launches instead of five:
-//   nms_compact  a lane per row from the yv7_row_best records: rows with obj > conf and best
-//                obj*cls > conf append one 64-bit key ((~conf bits) << 32 | row) to their image's list
-//                (wave-aggregated atomic slot; list order is arbitrary — the key carries the
-//                reference's tie order, the row index, so sorting restores it exactly)
-//   nms_fast     one workgroup per image: bitonic sort of the keys in LDS, then a LAZY greedy scan in
-//                sorted order, 64 candidates at a time: each candidate is tested against every box
-//                already kept (IoU > thr, class-offset boxes) and against the earlier members of its
-//                block (64 x 64 mask, resolved by one wave with bit operations).  A candidate survives
-//                iff no earlier KEPT box overlaps it — exactly torchvision's greedy definition — so the
-//                scan touches only the sorted prefix that reaches max_det (for typical frames about
-//                max_det candidates), never the whole list.
+// ONE launch, one 1024-thread workgroup per image:
+//   1. compaction: the image's yv7_row_best records (a 16-byte read per anchor row) -> rows with
+//      obj > conf and best obj*cls > conf (:637/:653, :684) append a 64-bit sort key
+//      ((~conf bits) << 32 | row) through an LDS counter; list order is arbitrary — the key carries
+//      the reference's tie order (the row index), so sorting restores it exactly
+//   2. sort: bitonic over P = pow2 >= max(n, 1024) keys held in registers (P / 1024 per thread):
+//      partners within a wave by lane shuffles, across waves through LDS, across a thread's own
+//      keys in registers — the barriers are only the cross-wave stages' (14 of 66 at P = 2048)
+//   3. LAZY greedy in sorted order, 64 candidates at a time: each candidate against every box already
+//      kept (IoU > thr, class-offset boxes :702-703) and against the earlier members of its block
+//      (64 x 64 mask, resolved by one wave with bit operations).  A candidate survives iff no earlier
+//      KEPT box overlaps it — torchvision's greedy definition — so only the sorted prefix that reaches
+//      max_det (:705-706) is touched (for typical frames about max_det candidates)
+//   4. the output's padding rows (det 0, src_row -1)
+// More than FAST_LDS_KEYS candidates (rare in single-label mode) sort in global memory instead.
 struct FastArgs {
   const float* z;
   const RowBest* rb;
   int B, N, no;
   float conf, iou;
   int agnostic, max_det, max_nms;
-  size_t kcap;        // per-image key capacity (pow2 >= N)
-  uint64_t* keys;     // [B][kcap]
-  int* ncand;         // [B]
+  size_t kcap;        // per-image global key capacity (pow2 >= N)
+  uint64_t* keys;     // [B][kcap] (large candidate lists only)
   float* det;
   int64_t* src_row;
   int32_t* count;
 };
 
 constexpr int FAST_MAX_DET = 1024;   // kept-box list in LDS
+constexpr int FAST_LDS_KEYS = 8192;  // register / LDS sort capacity
 
-__global__ __launch_bounds__(NT) void nms_compact(const FastArgs a) {
-  const int b = blockIdx.y;
-  const int lane = threadIdx.x & 63;
-  const RowBest* rb = a.rb + (size_t)b * a.N;
-  uint64_t* keys = a.keys + (size_t)b * a.kcap;
-  for (int r0 = blockIdx.x * NT + (threadIdx.x & ~63); r0 < a.N; r0 += gridDim.x * NT) {
-    const int row = r0 + lane;
-    bool c = false;
-    float conf = 0.f;
-    if (row < a.N) {
-      const RowBest r = rb[row];
-      c = r.obj > a.conf && r.conf > a.conf;   // :637 / :653 then :684
-      conf = r.conf;
-    }
-    const uint64_t m = __ballot(c);
-    if (!m) continue;
-    int base = 0;
-    if (lane == 0) base = atomicAdd(a.ncand + b, __popcll(m));
-    base = __shfl(base, 0);
-    if (c) {
-      const int k = base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
-      keys[k] = ((uint64_t)(~__float_as_uint(conf)) << 32) | (uint32_t)row;
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int m) {
+  const int lo = __shfl_xor((int)(uint32_t)v, m, 64), hi = __shfl_xor((int)(uint32_t)(v >> 32), m, 64);
+  return ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo;
+}
+
+// Bitonic sort of E * 1024 keys, element i = e * 1024 + tid in r[e]; xl: LDS exchange buffer.
+template <int E>
+__device__ __forceinline__ void reg_bitonic(uint64_t (&r)[E], uint64_t* xl, int tid) {
+  constexpr int P = E * SORT_T;
+  const int lane = tid & 63;
+  for (int k = 2; k <= P; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      if (j >= SORT_T) {            // partner in this thread: slot e ^ (j / 1024)
+        const int je = j / SORT_T;
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          if (e & je) continue;
+          const int i = e * SORT_T + tid;
+          const bool asc = (i & k) == 0;
+          const uint64_t a = r[e], c = r[e | je];
+          const bool sw = (a > c) == asc;
+          r[e] = sw ? c : a;
+          r[e | je] = sw ? a : c;
+        }
+      } else if (j >= 64) {         // partner in another wave: through LDS
+#pragma unroll
+        for (int e = 0; e < E; ++e) xl[e * SORT_T + tid] = r[e];
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = e * SORT_T + tid;
+          const uint64_t p = xl[i ^ j];
+          const bool keep_min = ((i & k) == 0) == ((i & j) == 0);
+          r[e] = keep_min ? (p < r[e] ? p : r[e]) : (p > r[e] ? p : r[e]);
+        }
+        __syncthreads();
+      } else {                      // partner in this wave
+#pragma unroll
+        for (int e = 0; e < E; ++e) {
+          const int i = e * SORT_T + tid;
+          const uint64_t p = shfl_xor64(r[e], j);
+          const bool keep_min = ((i & k) == 0) == ((lane & j) == 0);
+          r[e] = keep_min ? (p < r[e] ? p : r[e]) : (p > r[e] ? p : r[e]);
+        }
+      }
     }
   }
+#pragma unroll
+  for (int e = 0; e < E; ++e) xl[e * SORT_T + tid] = r[e];
+  __syncthreads();
+}
+
+template <int E>
+__device__ __forceinline__ void sort_lds(uint64_t* skeys, int n, int tid) {
+  uint64_t r[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) {
+    const int i = e * SORT_T + tid;
+    r[e] = i < n ? skeys[i] : ~0ull;
+  }
+  __syncthreads();
+  reg_bitonic<E>(r, skeys, tid);
 }
 
 __global__ __launch_bounds__(SORT_T) void nms_fast(const FastArgs a) {
   const int b = blockIdx.x;
-  const int n = min(a.ncand[b], a.N);
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   constexpr int NW = SORT_T / 64;
   extern __shared__ __attribute__((aligned(16))) unsigned char fsm[];
-  uint64_t* skeys = reinterpret_cast<uint64_t*>(fsm);                              // [LDS_SORT_MAX]
-  float4* kbox = reinterpret_cast<float4*>(fsm + LDS_SORT_MAX * 8);                 // kept boxes (offset)
+  uint64_t* skeys = reinterpret_cast<uint64_t*>(fsm);                              // [FAST_LDS_KEYS]
+  float4* kbox = reinterpret_cast<float4*>(fsm + FAST_LDS_KEYS * 8);                // kept boxes (offset)
   float* karea = reinterpret_cast<float*>(kbox + FAST_MAX_DET);
   __shared__ float4 bbox[64], braw[64];
   __shared__ float barea[64], bconf[64];
   __shared__ int bcls[64], brow[64];
   __shared__ uint64_t sup[64];
   __shared__ unsigned char pre[64];
-  __shared__ int total_s;
+  __shared__ int total_s, n_s;
 
-  // ---- sort: keys ascending = (conf descending, row ascending), torchvision's stable order
-  int P = 1;
-  while (P < n) P <<= 1;
-  uint64_t* keys = a.keys + (size_t)b * a.kcap;
-  const bool in_lds = P <= LDS_SORT_MAX;
-  uint64_t* s = in_lds ? skeys : keys;
-  if (in_lds) {
-    for (int i = tid; i < P; i += SORT_T) skeys[i] = i < n ? keys[i] : ~0ull;
-  } else {
-    for (int i = n + tid; i < P; i += SORT_T) keys[i] = ~0ull;   // kcap >= P (pow2 >= N >= n)
+  // ---- 1. compaction
+  if (tid == 0) n_s = 0;
+  __syncthreads();
+  const RowBest* rb = a.rb + (size_t)b * a.N;
+  uint64_t* gkeys = a.keys + (size_t)b * a.kcap;
+  // a wave's rows r0 + u * NW * 64 + lane, U record loads in flight before any is used
+  constexpr int U = 8;
+  for (int r0 = wv * 64; r0 < a.N; r0 += U * NW * 64) {
+    RowBest rr[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = r0 + u * NW * 64 + lane;
+      rr[u] = row < a.N ? rb[row] : RowBest{0.f, 0.f, 0, 0};
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int row = r0 + u * NW * 64 + lane;
+      const bool c = row < a.N && rr[u].obj > a.conf && rr[u].conf > a.conf;
+      const uint64_t m = __ballot(c);
+      if (!m) continue;
+      int base = 0;
+      if (lane == 0) base = atomicAdd(&n_s, __popcll(m));
+      base = __shfl(base, 0);
+      if (c) {
+        const int k = base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
+        const uint64_t key = ((uint64_t)(~__float_as_uint(rr[u].conf)) << 32) | (uint32_t)row;
+        if (k < FAST_LDS_KEYS) skeys[k] = key;
+        gkeys[k] = key;   // (the global copy is read only when the list outgrows the LDS sort)
+      }
+    }
   }
   __syncthreads();
-  if (in_lds) {
+  const int n = n_s;
+  // ---- 2. sort: keys ascending = (conf descending, row ascending), torchvision's stable order
+  const uint64_t* s = skeys;
+  if (n <= SORT_T) sort_lds<1>(skeys, n, tid);
+  else if (n <= 2 * SORT_T) sort_lds<2>(skeys, n, tid);
+  else if (n <= 4 * SORT_T) sort_lds<4>(skeys, n, tid);
+  else if (n <= FAST_LDS_KEYS) sort_lds<8>(skeys, n, tid);
+  else {   // global bitonic over the whole list
+    int P = 1;
+    while (P < n) P <<= 1;
+    for (int i = n + tid; i < P; i += SORT_T) gkeys[i] = ~0ull;
+    __syncthreads();
     for (int k = 2; k <= P; k <<= 1)
       for (int j = k >> 1; j > 0; j >>= 1) {
         for (int i = tid; i < P; i += SORT_T) {
           const int ixj = i ^ j;
           if (ixj > i) {
-            const uint64_t ki = skeys[i], kj = skeys[ixj];
-            if ((ki > kj) == ((i & k) == 0)) { skeys[i] = kj; skeys[ixj] = ki; }
+            const uint64_t ki = gkeys[i], kj = gkeys[ixj];
+            if ((ki > kj) == ((i & k) == 0)) { gkeys[i] = kj; gkeys[ixj] = ki; }
           }
         }
         __syncthreads();
       }
-  } else {
-    for (int k = 2; k <= P; k <<= 1)
-      for (int j = k >> 1; j > 0; j >>= 1) {
-        for (int i = tid; i < P; i += SORT_T) {
-          const int ixj = i ^ j;
-          if (ixj > i) {
-            const uint64_t ki = keys[i], kj = keys[ixj];
-            if ((ki > kj) == ((i & k) == 0)) { keys[i] = kj; keys[ixj] = ki; }
-          }
-        }
-        __syncthreads();   // (global keys: one workgroup, its own L1/L2 view; the fence orders them)
-      }
+    s = gkeys;
   }
+  // ---- 3. lazy greedy
   const int m = n < a.max_nms ? n : a.max_nms;   // :698-699 (first max_nms in sorted order)
   if (tid == 0) total_s = 0;
   __syncthreads();
   const float* zb = a.z + (size_t)b * a.N * a.no;
-  const RowBest* rb = a.rb + (size_t)b * a.N;
+  // wave 0 holds the next block's candidate in registers (lane = candidate): its z box and class are
+  // loaded one block ahead, so their latency sits under the current block's IoU work
+  float4 nz = make_float4(0.f, 0.f, 0.f, 0.f);
+  int ncls = 0, nrow = 0;
+  float nconf = 0.f;
+  auto fetch = [&](int base) {
+    const int j = base + tid;
+    if (tid < 64 && j < m) {
+      const uint64_t key = s[j];
+      nrow = (int)(uint32_t)key;
+      nconf = __uint_as_float(~(uint32_t)(key >> 32));
+      const float* zr = zb + (size_t)nrow * a.no;
+      nz = make_float4(zr[0], zr[1], zr[2], zr[3]);
+      ncls = rb[nrow].cls;
+    }
+  };
+  fetch(0);
   for (int base = 0; base < m; base += 64) {
-    // (1) the block's 64 candidates: boxes from z (xywh2xyxy, general.py:275-282), class from the row
-    //     record, class offset (general.py:702-703) unless agnostic
+    // the block's 64 candidates: boxes from z (xywh2xyxy, general.py:275-282), class from the row
+    // record, class offset (general.py:702-703) unless agnostic
     if (tid < 64) {
       const int j = base + tid;
       if (j < m) {
-        const uint64_t key = s[j];
-        const int row = (int)(uint32_t)key;
-        const float conf = __uint_as_float(~(uint32_t)(key >> 32));
-        const float* zr = zb + (size_t)row * a.no;
-        const float cx = zr[0], cy = zr[1], w = zr[2], h = zr[3];
+        const float cx = nz.x, cy = nz.y, w = nz.z, h = nz.w;
         float4 r;
         r.x = cx - w / 2.0f;
         r.y = cy - h / 2.0f;
         r.z = cx + w / 2.0f;
         r.w = cy + h / 2.0f;
-        const int cls = rb[row].cls;
-        const float off = a.agnostic ? 0.0f : (float)cls * (float)MAX_WH;
+        const float off = a.agnostic ? 0.0f : (float)ncls * (float)MAX_WH;
         float4 bx;
         bx.x = r.x + off;
         bx.y = r.y + off;
@@ -627,15 +699,16 @@ __global__ __launch_bounds__(SORT_T) void nms_fast(const FastArgs a) {
         braw[tid] = r;
         bbox[tid] = bx;
         barea[tid] = (bx.z - bx.x) * (bx.w - bx.y);
-        bconf[tid] = conf;
-        bcls[tid] = cls;
-        brow[tid] = row;
+        bconf[tid] = nconf;
+        bcls[tid] = ncls;
+        brow[tid] = nrow;
       }
+      fetch(base + 64);
     }
     __syncthreads();
     const int total = total_s;
-    // (2) each wave: its 4 block rows i against the later block members (lanes) -> sup[i]; and its 4
-    //     candidates against every kept box so far -> pre[i] (suppressed by an earlier kept box)
+    // each wave: its 4 block rows i against the later block members (lanes) -> sup[i]; and its 4
+    // candidates against every kept box so far -> pre[i] (suppressed by an earlier kept box)
 #pragma unroll
     for (int q = 0; q < 64 / NW; ++q) {
       const int i = wv * (64 / NW) + q;
@@ -657,7 +730,7 @@ __global__ __launch_bounds__(SORT_T) void nms_fast(const FastArgs a) {
       }
     }
     __syncthreads();
-    // (3) wave 0 resolves the block in order
+    // wave 0 resolves the block in order
     if (tid < 64) {
       const int j = base + lane;
       const bool valid = j < m && !pre[lane];
@@ -691,7 +764,15 @@ __global__ __launch_bounds__(SORT_T) void nms_fast(const FastArgs a) {
     __syncthreads();
     if (total_s >= a.max_det) break;   // :705-706
   }
-  if (tid == 0) a.count[b] = total_s < a.max_det ? total_s : a.max_det;
+  // ---- 4. padding rows
+  const int cnt = total_s < a.max_det ? total_s : a.max_det;
+  for (int di = cnt + tid; di < a.max_det; di += SORT_T) {
+    float* d = a.det + ((size_t)b * a.max_det + di) * 6;
+#pragma unroll
+    for (int q = 0; q < 6; ++q) d[q] = 0.0f;
+    a.src_row[(size_t)b * a.max_det + di] = -1;
+  }
+  if (tid == 0) a.count[b] = cnt;
 }
 
 struct Layout {
@@ -803,12 +884,10 @@ hipError_t launch_nms(const float* z, const void* rowbest, int B, int N, int no,
   a.src_row = src_row;
   a.count = count;
   hipError_t e;
-  if ((e = hipMemsetAsync(det, 0, sizeof(float) * 6 * (size_t)B * max_det, st)) != hipSuccess) return e;
-  if ((e = hipMemsetAsync(src_row, 0xff, sizeof(int64_t) * (size_t)B * max_det, st)) != hipSuccess) return e;
   int gx = (N + NT - 1) / NT;   // a lane per row
   if (gx > 1024) gx = 1024;
   if (!a.multi && !classes && !per_class && max_det <= FAST_MAX_DET) {
-    // fast path (single label, no class filter): compact -> sort + lazy greedy
+    // fast path (single label, no class filter): one launch (+ the row records when z comes alone)
     FastArgs f;
     f.z = z;
     f.rb = reinterpret_cast<const RowBest*>(rowbest);
@@ -830,14 +909,10 @@ hipError_t launch_nms(const float* z, const void* rowbest, int B, int N, int no,
     f.max_nms = max_nms;
     f.kcap = L.kcap;
     f.keys = reinterpret_cast<uint64_t*>(w + L.fkeys);
-    f.ncand = a.ncand;
     f.det = det;
     f.src_row = src_row;
     f.count = count;
-    if ((e = hipMemsetAsync(a.ncand, 0, sizeof(int) * (size_t)B, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(nms_compact, dim3(gx, B), dim3(NT), 0, st, f);
-    if ((e = hipGetLastError()) != hipSuccess) return e;
-    const size_t lds = sizeof(uint64_t) * LDS_SORT_MAX + (sizeof(float4) + sizeof(float)) * FAST_MAX_DET;
+    const size_t lds = sizeof(uint64_t) * FAST_LDS_KEYS + (sizeof(float4) + sizeof(float)) * FAST_MAX_DET;
     static bool fast_attr = false;
     if (!fast_attr) {
       if ((e = hipFuncSetAttribute((const void*)nms_fast, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)) !=
@@ -848,6 +923,8 @@ hipError_t launch_nms(const float* z, const void* rowbest, int B, int N, int no,
     hipLaunchKernelGGL(nms_fast, dim3(B), dim3(SORT_T), lds, st, f);
     return hipGetLastError();
   }
+  if ((e = hipMemsetAsync(det, 0, sizeof(float) * 6 * (size_t)B * max_det, st)) != hipSuccess) return e;
+  if ((e = hipMemsetAsync(src_row, 0xff, sizeof(int64_t) * (size_t)B * max_det, st)) != hipSuccess) return e;
   if (rowbest && !a.multi && !classes)
     hipLaunchKernelGGL(nms_rows_from_best, dim3(gx, B), dim3(NT), 0, st, a, reinterpret_cast<const RowBest*>(rowbest));
   else
