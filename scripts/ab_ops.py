@@ -29,6 +29,8 @@ ap.add_argument('--rounds', type=int, default=3)
 ap.add_argument('--iters', type=int, default=4)
 ap.add_argument('--out', default='')
 ap.add_argument('--ops', default='', help='comma-separated op indices to force (default: every CONV op)')
+ap.add_argument('--fp8', type=int, default=None, help='fp8 plan (this min_cout; 0 = every eligible 1x1): forces '
+                'only its fp8 ops (variants 0 = fused quantization, 81 = staged) and adds the fp16 time column')
 a = ap.parse_args()
 variants = [int(v) for v in a.variants.split(',')]
 m = Model(a.model)
@@ -39,6 +41,17 @@ B, H = a.b, a.img
 x = torch.rand(B, 3, H, H, device='cuda:0').half()
 z = torch.empty(B, plan.num_rows(H, H), plan.no, device='cuda:0')
 convs = [i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV]
+f16_us = None
+if a.fp8 is not None:
+    plan.profile_enable(a.iters)
+    for _ in range(a.iters + 2):
+        plan.forward_into(x, z)
+    torch.cuda.synchronize()
+    n, ms = plan.profile_read()
+    f16_us = [t / n * 1e3 for t in ms]
+    plan = Plan.fp8_from_model(m.half().to('cuda:0'), 'cuda:0', min_cout=a.fp8)
+    assert len(plan.graph.ops) == len(f16_us)
+    convs = [i for i, o in enumerate(plan.graph.ops) if o.get('wfmt', 0) == L.WFMT_FP8]
 if a.ops:
     convs = [int(v) for v in a.ops.split(',')]
 times = {v: {i: [] for i in range(len(plan.graph.ops))} for v in variants}
@@ -71,11 +84,17 @@ for i, o in enumerate(plan.graph.ops):
     best = variants[min(range(len(ts)), key=lambda k: ts[k])] if i in convs else variants[0]
     tot_best += med[best][i]
     rows.append({'op': i, 'desc': desc, 'us': dict(zip(variants, ts)), 'best': best})
-    if i in convs or not a.ops:
-        print(f'{i:3d} {desc:34s} ' + ' '.join(f'{t:8.1f}' for t in ts) + f'   {best}')
+    if f16_us is not None:
+        rows[-1]['f16_us'] = f16_us[i]
+    if i in convs or not (a.ops or f16_us):
+        print(f'{i:3d} {desc:34s} ' + ' '.join(f'{t:8.1f}' for t in ts) + f'   {best}' +
+              (f'   f16 {f16_us[i]:8.1f}' if f16_us else ''))
 print(f'forward (sum of ops): default {tot_def / 1e3:.3f} ms, best per op {tot_best / 1e3:.3f} ms')
 for v in variants:
     print(f'  variant {v}: {sum(med[v].values()) / 1e3:.3f} ms')
+if f16_us:
+    print(f'  fp16 plan: {sum(f16_us) / 1e3:.3f} ms; fp8 ops only: f16 {sum(f16_us[i] for i in convs) / 1e3:.3f} ms, '
+          + ', '.join(f'v{v} {sum(med[v][i] for i in convs) / 1e3:.3f} ms' for v in variants))
 if a.out:
     with open(a.out, 'w') as f:
         json.dump({'model': a.model, 'b': B, 'img': H, 'variants': variants, 'rows': rows,

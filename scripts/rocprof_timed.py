@@ -7,6 +7,7 @@ weight-stationary 3x3, halo, tile kernels) over the timed forwards and over the 
 of them (the ones bench.py's live HIP events covered), and the NMS kernels' durations per batch.
 usage: python scripts/rocprof_timed.py <kernel_trace.csv> <bench.json> [out.json]"""
 import csv
+import re
 import json
 import statistics
 import sys
@@ -40,7 +41,7 @@ res = {'forwards_in_trace': fwd + 1, 'timed_forwards': len(timed),
        'conv_mean_us_live_forwards': round(statistics.mean(conv_live), 2) if conv_live else None,
        'bench_events_mean_launch_us': bench['roofline']['mean_launch_us'],
        'nms_kernels_us_per_batch_timed': round(statistics.median(nms), 1) if nms else None,
-       'nms_kernels': sorted({r['Kernel_Name'].split('(')[0].split('::')[-1] for r in rows
+       'nms_kernels': sorted({re.search(r'(nms_\w+|row_best\w*)', r['Kernel_Name']).group(1) for r in rows
                               if any(c in r['Kernel_Name'] for c in NMS)})}
 print(json.dumps(res, indent=1))
 if len(sys.argv) > 3:

@@ -113,10 +113,13 @@ def test_gpu_fp8_quantizer_bit_exact():
     B, H, W = 2, 128, 160
     x = frames(B, H, W, seed=5)
     plan = _gpu_fp8_plan('yolov7', x, 0)
+    ops = [i for i, o in enumerate(plan.graph.ops) if o.get('wfmt', 0) == L.WFMT_FP8]
+    for i in ops:
+        plan.set_op_variant(i, 81)   # the staged configuration: a separate quantize pass into the buffer
     z = torch.empty(B, plan.num_rows(H, W), plan.no, device='cuda:0')
     plan.forward_into(x.cuda().half(), z)
     torch.cuda.synchronize()
-    o = [o for o in plan.graph.ops if o.get('wfmt', 0) == L.WFMT_FP8][-1]
+    o = plan.graph.ops[ops[-1]]
     src = plan.tensor_view(o['src'], B, H, W)[..., o['src_coff']:o['src_coff'] + o['cin']].float().cpu()
     M, cin = src.numel() // o['cin'], o['cin']
     kp = (cin + 127) // 128 * 128
@@ -124,6 +127,29 @@ def test_gpu_fp8_quantizer_bit_exact():
     want[:, :cin] = (src.reshape(M, cin) / o['xscale']).clamp(-448.0, 448.0).to(torch.float8_e4m3fn).view(torch.uint8)
     got = plan.f8_scratch(B, H, W)[:M * kp].view(M, kp).cpu()
     assert torch.equal(got, want), int((got != want).sum())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name,B,H,W', [('yolov7', 2, 128, 160), ('yolov7-tiny', 3, 96, 224)])
+def test_gpu_fp8_fused_quantize_matches_staged(name, B, H, W):
+    """Variant 82 quantizes the fp16 input in registers on the way into LDS; variant 81 (staged) writes
+    the e4m3 copy with the separate, bit-exact quantizer first.  Same bytes in LDS, same MFMA order: the
+    two forwards agree bit for bit on every tensor (and the default dispatch mixes the two per layer)."""
+    x = frames(B, H, W, seed=12)
+    plan = _gpu_fp8_plan(name, x, 0)
+    ops = [i for i, o in enumerate(plan.graph.ops) if o.get('wfmt', 0) == L.WFMT_FP8]
+    xd = x.cuda().half()
+    for i in ops:
+        plan.set_op_variant(i, 82)
+    z0, r0 = plan.forward(xd)
+    t0 = [plan.tensor_view(t, B, H, W).clone() for t in range(len(plan.graph.tensors))]
+    for i in ops:
+        plan.set_op_variant(i, 81)
+    z1, r1 = plan.forward(xd)
+    torch.cuda.synchronize()
+    for t, a in enumerate(t0):
+        assert torch.equal(a, plan.tensor_view(t, B, H, W)), f'tensor {t}'
+    assert torch.equal(z0, z1) and all(torch.equal(a, b) for a, b in zip(r0, r1))
 
 
 @pytest.mark.gpu

@@ -76,7 +76,7 @@ __global__ __launch_bounds__(256) void quant_f8_kernel(const _Float16* __restric
 }
 
 // ---- persistent fp8 ring GEMM (1x1): M pixels x N = cout x K = kp
-template <int BM, int BN, int WM, int WN, int STAGES, int ACT>
+template <int BM, int BN, int WM, int WN, int STAGES, int ACT, bool XF16 = false>
 __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * ROWB8 <= 76 * 1024) ? 2 : 1) void conv_f8_kernel(
     const F8ConvParams p) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
@@ -107,8 +107,14 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * ROWB8 <= 76 * 1
   const int ntl = (T - (int)blockIdx.x + G - 1) / G;
   const int nsteps = ntl * nk;
 
-  const auto xr = make_rsrc(p.x8, (uint32_t)((size_t)p.M * p.kp));
+  const auto xr = XF16 ? make_rsrc(p.x16, p.xbytes) : make_rsrc(p.x8, (uint32_t)((size_t)p.M * p.kp));
   const auto wr = make_rsrc(p.w8, p.wbytes);
+  // XF16: this thread's activation pieces per K step: rows (tid >> 3) + 32 q, 16-channel chunk tid & 7
+  // (8 threads per row cover its 128 channels: 256 coalesced bytes of fp16 in, 128 bytes of e4m3 out)
+  constexpr int QR = XF16 ? BM / (NTH / 8) : 1;
+  uint32_t q_off[QR];
+  u4 q_lo[QR], q_hi[QR];
+  const int q_chunk = tid & 7, q_row0 = tid >> 3;
   const auto yr = make_rsrc(p.y, 0x7fffffffu);
 
   for (int i = tid; i < p.cout; i += NTH) {
@@ -122,10 +128,24 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * ROWB8 <= 76 * 1
     if (ikt == 0) {
       const int t = blockIdx.x + it * G;
       const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+      if constexpr (XF16) {
+        const int hw = p.H * p.W;
 #pragma unroll
-      for (int j = 0; j < RA; ++j) {
-        const int m = m0 + (j * NW + wave) * 8 + lr;
-        a_off[j] = m < p.M ? (uint32_t)m * p.kp + c * 16 : 0x80000000u;
+        for (int q = 0; q < QR; ++q) {
+          const int m = m0 + q_row0 + q * (NTH / 8);
+          if (m < p.M) {
+            const int b = m / hw, r = m - b * hw, h = r / p.W, w = r - h * p.W;
+            q_off[q] = (uint32_t)((pix_index(b, h, w, p.H, p.W) * p.xc + p.xoff + q_chunk * 16) * 2);
+          } else {
+            q_off[q] = 0x80000000u;   // past the buffer: zeros
+          }
+        }
+      } else {
+#pragma unroll
+        for (int j = 0; j < RA; ++j) {
+          const int m = m0 + (j * NW + wave) * 8 + lr;
+          a_off[j] = m < p.M ? (uint32_t)m * p.kp + c * 16 : 0x80000000u;
+        }
       }
 #pragma unroll
       for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)((n0 + (j * NW + wave) * 8 + lr) * p.kp + c * 16);
@@ -135,10 +155,49 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * ROWB8 <= 76 * 1
     const uint32_t so = (uint32_t)ikt * 128;
 #pragma unroll
     for (int j = 0; j < RB; ++j) dma16_f8(wr, As + (j * NW + wave) * 8 * ROWB8, b_off[j], so);
+    if constexpr (XF16) {
+      // channels [ikt * 128 + 16 chunk, + 16) of each row: two 16-byte fp16 loads (zeros past cin)
+      const int c0 = ikt * 128 + q_chunk * 16;
+      const bool lo_in = c0 < p.cin, hi_in = c0 + 8 < p.cin;
 #pragma unroll
-    for (int j = 0; j < RA; ++j) dma16_f8(xr, Bs + (j * NW + wave) * 8 * ROWB8, a_off[j], so);
+      for (int q = 0; q < QR; ++q) {
+        q_lo[q] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, lo_in ? q_off[q] : 0x80000000u,
+                                                                               (uint32_t)ikt * 256, 0));
+        q_hi[q] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, hi_in ? q_off[q] + 16 : 0x80000000u,
+                                                                               (uint32_t)ikt * 256, 0));
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < RA; ++j) dma16_f8(xr, Bs + (j * NW + wave) * 8 * ROWB8, a_off[j], so);
+    }
     ++ig;
     if (++ikt == nk) { ikt = 0; ++it; }
+  };
+  // XF16: the staged activation pieces of stage `slot` -> e4m3 -> LDS (the DMA image: row r, chunk
+  // slot swz8(r, chunk)), x * qscale clamped to +-448 and rounded by v_cvt_pk_fp8_f32 exactly as
+  // quant_f8_kernel does
+  auto commit_x = [&](int slot) {
+    unsigned char* Bs = smem + slot * STAGE + BN * ROWB8;
+#pragma unroll
+    for (int q = 0; q < QR; ++q) {
+      const int row = q_row0 + q * (NTH / 8);
+      const _Float16* a = reinterpret_cast<const _Float16*>(&q_lo[q]);
+      const _Float16* bq = reinterpret_cast<const _Float16*>(&q_hi[q]);
+      float v[16];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        v[e] = __builtin_fminf(__builtin_fmaxf((float)a[e] * p.qscale, -448.0f), 448.0f);
+        v[e + 8] = __builtin_fminf(__builtin_fmaxf((float)bq[e] * p.qscale, -448.0f), 448.0f);
+      }
+      u4 o;
+#pragma unroll
+      for (int d = 0; d < 4; ++d) {
+        int r = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * d], v[4 * d + 1], 0, false);
+        r = __builtin_amdgcn_cvt_pk_fp8_f32(v[4 * d + 2], v[4 * d + 3], r, true);
+        o[d] = (uint32_t)r;
+      }
+      *reinterpret_cast<u4*>(Bs + row * ROWB8 + swz8(row, q_chunk) * 16) = o;
+    }
   };
 
   f4 acc[TN][TM];
@@ -194,12 +253,57 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * ROWB8 <= 76 * 1
 #pragma unroll
   for (int s0 = 0; s0 < STAGES - 1; ++s0)
     if (ig < nsteps) issue_next();
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bias / scale LDS writes of this wave
+  if constexpr (XF16) {   // stage 0's activations: wait for its loads, quantize into LDS
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    commit_x(0);
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bias / scale (/ activation) LDS writes of this wave
   __builtin_amdgcn_s_barrier();
   init_tile(0);
 
   int ci = 0, ckt = 0;
   for (int gs = 0; gs < nsteps; ++gs) {
+    if constexpr (XF16) {
+      static_assert(STAGES == 2, "the staged activations cover one stage ahead");
+      // stage gs's weights landed and its activations were committed (by every wave: the barrier)
+      const bool st = ci > 0 && ckt == 0;
+      if (st) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(NST) : "memory");
+      else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
+      const bool more = ig < nsteps;
+      if (more) issue_next();   // stage gs+1: weight DMA + activation loads to registers
+      const unsigned char* As = smem + (gs % STAGES) * STAGE;
+      const unsigned char* Bs = As + BN * ROWB8;
+      v8i wa[TN], xb[TM];
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WTN + j * 16 + li;
+        const u4 q0 = *reinterpret_cast<const u4*>(As + row * ROWB8 + swz8(row, 2 * g) * 16);
+        const u4 q1 = *reinterpret_cast<const u4*>(As + row * ROWB8 + swz8(row, 2 * g + 1) * 16);
+        wa[j] = v8i{(int)q0[0], (int)q0[1], (int)q0[2], (int)q0[3], (int)q1[0], (int)q1[1], (int)q1[2], (int)q1[3]};
+      }
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) {
+        const int row = wm * WTM + ii * 16 + li;
+        const u4 q0 = *reinterpret_cast<const u4*>(Bs + row * ROWB8 + swz8(row, 2 * g) * 16);
+        const u4 q1 = *reinterpret_cast<const u4*>(Bs + row * ROWB8 + swz8(row, 2 * g + 1) * 16);
+        xb[ii] = v8i{(int)q0[0], (int)q0[1], (int)q0[2], (int)q0[3], (int)q1[0], (int)q1[1], (int)q1[2], (int)q1[3]};
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int ii = 0; ii < TM; ++ii)
+          acc[j][ii] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(wa[j], xb[ii], acc[j][ii], 0, 0, 0, 127, 0, 127);
+      __builtin_amdgcn_s_setprio(0);
+      if (more) commit_x((gs + 1) % STAGES);   // the slot every wave finished reading at step gs-1
+      if (++ckt == nk) {
+        epilogue();
+        ckt = 0;
+        if (++ci < ntl) init_tile(ci);
+      }
+      continue;
+    }
     // stage gs has landed once at most `younger` vector-memory ops of this wave are outstanding:
     // the next stage's pieces (if issued) and, right after a tile boundary, the epilogue's stores
     const int ndma = min(STAGES - 2, nsteps - 1 - gs);
@@ -246,15 +350,15 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * ROWB8 <= 76 * 1
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BM, int BN, int WM, int WN, int STAGES>
+template <int BM, int BN, int WM, int WN, int STAGES, bool XF16>
 hipError_t launch_f8(const F8ConvParams& p, int occ, hipStream_t st) {
   const long T = (long)((p.M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
   const long cap = (long)cu_count() * occ;
   const int grid = (int)(T < cap ? T : cap);
   const dim3 blk(64 * WM * WN);
-  if (p.act == 1) hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 1>), dim3(grid), blk, 0, st, p);
-  else if (p.act == 2) hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 2>), dim3(grid), blk, 0, st, p);
-  else hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 0>), dim3(grid), blk, 0, st, p);
+  if (p.act == 1) hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 1, XF16>), dim3(grid), blk, 0, st, p);
+  else if (p.act == 2) hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 2, XF16>), dim3(grid), blk, 0, st, p);
+  else hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 0, XF16>), dim3(grid), blk, 0, st, p);
   return hipGetLastError();
 }
 
@@ -278,7 +382,11 @@ hipError_t launch_conv_f8(const F8ConvParams& p, hipStream_t st) {
     return hipErrorInvalidValue;
   // 128 x 128 tiles, two 4-wave blocks per CU (a 256 x 256 tile's 32 fragment registers of 32 fp8 each
   // per operand do not fit beside its 128 accumulators: it spills)
-  return launch_f8<128, 128, 2, 2, 2>(p, 2, st);
+  if (!p.x8) {
+    if (!p.x16 || p.cin <= 0 || p.cin % 8 || p.xoff % 8 || p.xc % 8 || p.kp < p.cin) return hipErrorInvalidValue;
+    return launch_f8<128, 128, 2, 2, 2, true>(p, 2, st);
+  }
+  return launch_f8<128, 128, 2, 2, 2, false>(p, 2, st);
 }
 
 }  // namespace yv7

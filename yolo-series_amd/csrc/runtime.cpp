@@ -353,8 +353,10 @@ int yv7_workspace_forget(yv7_plan* p, const void* ws, size_t bytes) {
 // Kernel variants a caller may force per op: every real kernel configuration of the fp16 dispatch
 // (conv_f16.hip launch_conv_f16 / choose), never the microbenchmark hooks (90-99, 298; ws64's 12-14
 // and 16), which skip work on purpose.
-static bool variant_allowed(int kind, int v) {
+static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (v == 0) return true;
+  const int kind = o.kind;
+  if (is_f8(o)) return v == 81 || v == 82;   // fp8 1x1: staged quantize pass / fused quantization
   if (kind == YV7_OP_DETECT) return v == 92 || v == 97;
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
@@ -366,7 +368,7 @@ int yv7_set_op_variant(yv7_plan* p, int op, int variant) {
   const auto& o = p->ops[op];
   if (o.kind != YV7_OP_CONV && o.kind != YV7_OP_DETECT)
     return fail(YV7_E_ARG, "yv7_set_op_variant: op " + std::to_string(op) + " is not a CONV / DETECT op");
-  if (!variant_allowed(o.kind, variant))
+  if (!variant_allowed(o, variant))
     return fail(YV7_E_ARG, "yv7_set_op_variant: variant " + std::to_string(variant) + " is not a kernel configuration");
   p->op_variant[op] = variant;
   return 0;
@@ -491,12 +493,30 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
           c.yc = to.channels;
           c.yoff = o.dst_coff;
           if (is_f8(o)) {
-            // quantize the input slice to the dense e4m3 staging buffer, then the fp8 GEMM
-            unsigned char* x8 = wsb + scr.f8_off;
-            e = yv7::launch_quant_f8(c.x, B, c.H, c.W, c.xc, c.xoff, o.cin, c.kpad, 1.0f / o.xscale, x8, st);
-            if (e != hipSuccess) return hip_fail(e, "yv7_forward fp8 quantize");
+            // 82: the fp8 GEMM quantizes the fp16 input slice on its way into LDS (no staging pass, but
+            // every N tile of a row block converts it again: VALU work ~2x the block's MFMA time per
+            // K step); 81: a separate quantize pass into the dense e4m3 staging buffer, then the GEMM
+            // reads e4m3 by LDS-DMA.  Default (measured per layer on MI355X, bs32 640, profiles/
+            // r2_fp8_ab_*.txt): fused up to 2 N tiles (cout <= 256), staged beyond.
             yv7::F8ConvParams f;
-            f.x8 = x8;
+            std::memset(&f, 0, sizeof(f));
+            const int v = p->op_variant[i];
+            if (v == 81 || (v == 0 && o.cout > 256)) {
+              unsigned char* x8 = wsb + scr.f8_off;
+              e = yv7::launch_quant_f8(c.x, B, c.H, c.W, c.xc, c.xoff, o.cin, c.kpad, 1.0f / o.xscale, x8, st);
+              if (e != hipSuccess) return hip_fail(e, "yv7_forward fp8 quantize");
+              f.x8 = x8;
+            } else {
+              const size_t xb = yv7::bordered_pixels(B, c.H, c.W) * c.xc * 2;
+              if (xb >= ((size_t)1 << 31))
+                return fail(YV7_E_SHAPE, "yv7_forward: fp8 op " + std::to_string(i) + " input exceeds 2 GiB");
+              f.x16 = c.x;
+              f.xbytes = (uint32_t)xb;
+              f.xc = c.xc;
+              f.xoff = c.xoff;
+              f.cin = o.cin;
+              f.qscale = 1.0f / o.xscale;
+            }
             f.y = c.y;
             f.w8 = c.w;
             f.bias = c.bias;

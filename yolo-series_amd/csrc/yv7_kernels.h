@@ -96,6 +96,13 @@ struct F8ConvParams {
   float xscale;         // activation scale: x ~ e4m3 value * xscale
   uint32_t wbytes;      // byte size of w8 (buffer range)
   int M, kp, cout, H, W, yc, yoff, act;   // H, W: output (= input) interior size
+  // fused quantization (x8 == nullptr): the fp16 input slice [xoff, xoff + cin) of the bordered NHWC
+  // tensor x16 (pitch xc, xbytes long) is quantized to e4m3 (x * qscale, clamped to +-448) on its
+  // way into LDS, so no dense e4m3 copy is written first
+  const void* x16;
+  uint32_t xbytes;
+  int xc, xoff, cin;
+  float qscale;
 };
 hipError_t launch_quant_f8(const void* x, int B, int H, int W, int xc, int xoff, int cin, int kp, float qscale,
                            void* y8, hipStream_t st);
