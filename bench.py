@@ -478,7 +478,15 @@ def main(argv=None):
                          # whole job: images/s against the layer-boundary HBM ceiling of the whole forward
                          # (17 625 img/s for yolov7 640 bs32 fp16)
                          'job_ceiling_images_per_s': round(job_ceiling, 1),
-                         'job_frac': round(value / world / job_ceiling, 4)},
+                         'job_frac': round(value / world / job_ceiling, 4),
+                         # the same family over the timed region as a whole: its algorithmic bytes per
+                         # step / ms_per_step.  With S batches in flight a launch shares the chip with
+                         # the other streams' launches, so per-launch durations (`achieved`) count
+                         # overlapped time S-fold at most; `overlap` = summed launch time / step time
+                         'family_stream_gbs': round(nconv * bytes_per_launch / (elapsed / a.steps) / 1e9, 1),
+                         'family_stream_frac': round(nconv * bytes_per_launch / (elapsed / a.steps) / 1e9
+                                                     / HBM_PEAK_GBS, 4),
+                         'overlap': round(conv_ms / 1e3 / (elapsed / a.steps), 2) if nf else None},
             'detail': {'forward_ms_events': round(fwd_ms, 3), 'conv_ms_events': round(conv_ms, 3),
                        'serial_conv_launch_us': round(serial[0] * 1e6, 2),
                        'serial_conv_frac': round(serial[1] / serial[0] / 1e9 / HBM_PEAK_GBS, 4),

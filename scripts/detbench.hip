@@ -4,6 +4,7 @@
 //        -L yolo-series_amd/yv7 -lyv7 -Wl,-rpath,$PWD/yolo-series_amd/yv7 -o scripts/detbench
 #include <hip/hip_runtime.h>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 #include "yv7_kernels.h"
@@ -18,9 +19,21 @@ int main(int argc, char** argv) {
   CK(hipMalloc(&z, (size_t)B * nrows * no * 4)); CK(hipMalloc(&best, (size_t)B * nrows * 16));
   CK(hipMalloc(&x, yv7::bordered_pixels(B, 80, 80) * 256 * 2)); CK(hipMalloc(&w, 256 * 1024 * 2));
   CK(hipMalloc(&b, 256 * 4)); CK(hipMalloc(&zero, 4096));
-  CK(hipMemset(x, 0, yv7::bordered_pixels(B, 80, 80) * 256 * 2)); CK(hipMemset(w, 0, 256 * 1024 * 2));
+  {   // random operands (zeros would let the chip hold a higher clock than real data)
+    const size_t nx = yv7::bordered_pixels(B, 80, 80) * 256, nw = 256 * 1024;
+    std::vector<_Float16> hx(nx), hw(nw);
+    uint32_t s = 12345u;
+    for (auto& v : hx) { s = s * 1664525u + 1013904223u; v = (_Float16)(((s >> 8) & 0xffff) / 65536.0f - 0.5f); }
+    for (auto& v : hw) { s = s * 1664525u + 1013904223u; v = (_Float16)((((s >> 8) & 0xffff) / 65536.0f - 0.5f) * 0.1f); }
+    CK(hipMemcpy(x, hx.data(), nx * 2, hipMemcpyHostToDevice));
+    CK(hipMemcpy(w, hw.data(), nw * 2, hipMemcpyHostToDevice));
+  }
   CK(hipMemset(b, 0, 256 * 4)); CK(hipMemset(zero, 0, 4096));
   std::vector<int> variants = {0, 92, 97};
+  if (argc > 1) {   // e.g. 0,90,91,93,94 (hooks: 90 GEMM only, 91 epilogue only, 93 no z / row-score stores, 94 no K loop)
+    variants.clear();
+    for (char* t = strtok(argv[1], ","); t; t = strtok(nullptr, ",")) variants.push_back(atoi(t));
+  }
   int row_off = 0;
   hipEvent_t e0, e1; CK(hipEventCreate(&e0)); CK(hipEventCreate(&e1));
   for (auto& l : lv) {

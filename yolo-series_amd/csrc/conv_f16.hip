@@ -1204,6 +1204,243 @@ __global__ __launch_bounds__(64 * WM * WN, (2 * (BM + BN) * 128 <= 76 * 1024) ? 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// ---------------------------------------------------------------------------------------------
+// 8-phase persistent ring (256 x 256 tiles, 8 waves = 2 stagger groups x 4, BK 64): the structure of
+// the guide's 256^2 "8-phase" GEMM template (cdna_hip_programming.md §5: counted vmcnt across raw
+// barriers, one half-tile of LDS-DMA per phase, two wave groups offset by one barrier so that one
+// group's MFMA cluster runs while the other issues its LDS reads and DMA), rebuilt for the implicit
+// GEMM of a conv and made persistent across output tiles like conv_f16_pring_kernel.
+//
+//  * LDS: two K-tile buffers, each four 16 KiB half-tiles [A0 A1 B0 B1] (A = 128 pixel rows,
+//    B = 128 weight rows, 64 k each, XOR-swizzled 128-byte rows as everywhere here) + the bias.
+//  * K-tile k runs four phases, one block quadrant (ha, hb) each in the order (0,0) (0,1) (1,1) (1,0):
+//    every wave computes its 64 x 32 part of the quadrant (16 MFMAs), reading A half ha (8
+//    ds_read_b128) and/or B half hb (4): phase 0 both, then B1, A1, B0 — so the halves' last reads
+//    fall in phases 0 (A0), 1 (B1), 2 (A1), 3 (B0).
+//  * a half is restaged two phases after its last read (the WAR distance with the stagger), so
+//    phase 0 stages A1 of k+1, phase 1 B0 of k+1, phase 2 A0 of k+2, phase 3 B1 of k+2; the only
+//    wait is phase 3's vmcnt(4): K-tile k+1 retired, k+2's first two halves still in flight, and
+//    the reads of k+1 start one phase (and so one more barrier of the other group) later.
+//  * the finished tile's epilogue (bias in the accumulators, activation, fp16, permlane16 pairing,
+//    16-byte NHWC stores) runs between the last K-tile's phase 3 and the next tile's phase 0.
+// acc[hb][j][ha][i] = channels hb*128 + wn*32 + j*16 + g*4 + e of pixel ha*128 + wm*64 + i*16 + li.
+template <bool ONE, int ACT>
+__global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p) {
+  constexpr int BM = 256, BN = 256, NTH = 512;
+  constexpr int HALF = 128 * 128;                    // bytes per half-tile
+  constexpr int BUF = 4 * HALF;                      // one K-tile: A0 A1 B0 B1
+  constexpr int NST = 16;                            // epilogue stores per lane per tile
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + 4096];
+  float* bias_l = reinterpret_cast<float*>(smem + 2 * BUF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;           // wm: the stagger group
+  const int g = lane >> 4, li = lane & 15;
+  const int lr = lane >> 3;                          // DMA: row within an 8-row piece
+  const int c = (lane & 7) ^ lr;                     // DMA: source chunk of slot lane & 7
+
+  const int nN = (p.cout + BN - 1) / BN;
+  const int T = ((p.M + BM - 1) / BM) * nN;
+  const int G = gridDim.x;
+  const int nk = p.kpad / BKE;
+  const int ntl = (T - (int)blockIdx.x + G - 1) / G;
+  const int total = ntl * nk;                        // K-tiles this block computes
+
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto wr = make_rsrc(p.w, p.wbytes);
+  const auto yr = make_rsrc(p.y, 0x7fffffffu);
+  for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
+
+  // ---- staging cursors (A and B halves are staged in different phases, each in K-tile order)
+  int a_it = 0, a_kt = 0, b_it = 0, b_kt = 0, a_gk = 0, b_gk = 0;
+  uint32_t a_off[2][2], b_off[2][2], a_so = 0;
+  KCursor<BKE> su;
+  auto stage_a = [&](int h) {   // half h (0 / 1) of K-tile a_gk
+    if (h == 0) {
+      if (a_kt == 0) {
+        const int t = blockIdx.x + a_it * G;
+        PixelWalk pw(p, (t / nN) * BM + wave * 8 + lr);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q) pw.advance(p, 64);
+          a_off[q >> 1][q & 1] = a_origin(p, pw.b, pw.ho, pw.wo, c);
+        }
+        su.init(p, 0);
+      }
+      a_so = ONE ? (uint32_t)a_kt * BKE * 2 : su.offset(p);
+      if (!ONE) su.advance(p);
+    }
+    unsigned char* d = smem + (a_gk & 1) * BUF + h * HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(xr, d + (j * 8 + wave) * 8 * ROWB, a_off[h][j], a_so);
+    if (h == 1) {
+      ++a_gk;
+      if (++a_kt == nk) { a_kt = 0; ++a_it; }
+    }
+  };
+  auto stage_b = [&](int h) {   // half h of K-tile b_gk; staged B1 first, then B0
+    if (h == 1 && b_kt == 0) {
+      const int n0 = (blockIdx.x + b_it * G) % nN * BN;
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+        b_off[q >> 1][q & 1] = (uint32_t)(((n0 + (q >> 1) * 128 + ((q & 1) * 8 + wave) * 8 + lr) * p.kpad + c * 8) * 2);
+    }
+    unsigned char* d = smem + (b_gk & 1) * BUF + (2 + h) * HALF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(wr, d + (j * 8 + wave) * 8 * ROWB, b_off[h][j], (uint32_t)b_kt * BKE * 2);
+    if (h == 0) {
+      ++b_gk;
+      if (++b_kt == nk) { b_kt = 0; ++b_it; }
+    }
+  };
+
+  // ---- compute side
+  f4 acc[2][2][2][4];
+  int cm0 = 0, cn0 = 0;
+  auto init_tile = [&](int i) {
+    const int t = blockIdx.x + i * G;
+    cm0 = (t / nN) * BM;
+    cn0 = (t % nN) * BN;
+#pragma unroll
+    for (int hb = 0; hb < 2; ++hb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int col = cn0 + hb * 128 + wn * 32 + j * 16 + g * 4;
+        f4 bv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? bias_l[col + e] : 0.0f;
+#pragma unroll
+        for (int ha = 0; ha < 2; ++ha)
+#pragma unroll
+          for (int i = 0; i < 4; ++i) acc[hb][j][ha][i] = bv;
+      }
+  };
+  const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
+  auto epilogue = [&]() {
+#pragma unroll
+    for (int ha = 0; ha < 2; ++ha) {
+      PixelWalk pw(p, cm0 + ha * 128 + wm * 64 + li);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if (i) pw.advance(p, 16);
+        const int m = cm0 + ha * 128 + wm * 64 + i * 16 + li;
+        const uint32_t yo = (uint32_t)((pix_index(pw.b, pw.ho, pw.wo, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
+#pragma unroll
+        for (int hb = 0; hb < 2; ++hb) {
+          typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+          typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+          h4 va, vb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            va[e] = (_Float16)act_t<ACT>(acc[hb][0][ha][i][e]);
+            vb[e] = (_Float16)act_t<ACT>(acc[hb][1][ha][i][e]);
+          }
+          const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+          const u4 v = {s0[0], s1[0], s0[1], s1[1]};
+          const int n = cn0 + hb * 128 + wn * 32 + (int)lane_ch;
+          const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
+          __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+        }
+      }
+    }
+  };
+
+  // ---- prologue: K-tile 0 whole, K-tile 1's A0 and B1 in flight
+  stage_a(0); stage_b(1); stage_a(1); stage_b(0);
+  if (total > 1) {
+    stage_a(0); stage_b(1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bias_l
+  __builtin_amdgcn_s_barrier();
+  init_tile(0);
+  if (wm == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind group 0
+
+  u4 xa[2][4], wb[2][2];
+  auto read_a = [&](const unsigned char* h) {
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int row = wm * 64 + i * 16 + li;
+        xa[sb][i] = *reinterpret_cast<const u4*>(h + row * ROWB + swz(row, sb * 4 + g) * 16);
+      }
+  };
+  auto read_b = [&](const unsigned char* h) {
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int row = wn * 32 + j * 16 + li;
+        wb[sb][j] = *reinterpret_cast<const u4*>(h + row * ROWB + swz(row, sb * 4 + g) * 16);
+      }
+  };
+  auto mfma_q = [&](int ha, int hb) {
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[hb][j][ha][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[sb][j]),
+                                                                     __builtin_bit_cast(h8, xa[sb][i]),
+                                                                     acc[hb][j][ha][i], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+
+  int ci = 0, ckt = 0;
+  for (int k = 0; k < total; ++k) {
+    const unsigned char* bk = smem + (k & 1) * BUF;
+    const bool n1 = k + 1 < total, n2 = k + 2 < total;
+    // phase 0: quadrant (0,0)
+    read_b(bk + 2 * HALF);
+    read_a(bk);
+    if (n1) stage_a(1);
+    mfma_q(0, 0);
+    // phase 1: (0,1)
+    read_b(bk + 3 * HALF);
+    if (n1) stage_b(0);
+    mfma_q(0, 1);
+    // phase 2: (1,1)
+    read_a(bk + HALF);
+    if (n2) stage_a(0);
+    mfma_q(1, 1);
+    // phase 3: (1,0); K-tile k+1 retired (k+2's A0 and B1 may stay in flight)
+    read_b(bk + 2 * HALF);
+    if (n2) {
+      stage_b(1);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    mfma_q(1, 0);
+    if (++ckt == nk) {
+      epilogue();
+      ckt = 0;
+      if (++ci < ntl) init_tile(ci);
+    }
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts in both groups
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool ONE>
+hipError_t launch_p8_t(const ConvParams& p, int grid, hipStream_t st) {
+  if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1>), dim3(grid), dim3(512), 0, st, p);
+  else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 2>), dim3(grid), dim3(512), 0, st, p);
+  else hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 0>), dim3(grid), dim3(512), 0, st, p);
+  return hipGetLastError();
+}
+
 template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int BK>
 hipError_t launch_pring_act(const ConvParams& p, int grid, hipStream_t st) {
   if (p.act == 1)
@@ -1224,6 +1461,14 @@ int device_cus() {
     return v;
   }();
   return n;
+}
+
+// the 8-phase persistent ring: uniform K steps only (1x1, or cin % 64 == 0)
+hipError_t launch_p8(const ConvParams& p, bool one, hipStream_t st) {
+  if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || (!one && p.cin % BKE)) return hipErrorInvalidValue;
+  const long T = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
+  const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
+  return one ? launch_p8_t<true>(p, grid, st) : launch_p8_t<false>(p, grid, st);
 }
 
 template <int BM, int BN, int WM, int WN, bool ONE>
@@ -1432,6 +1677,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 221) return one ? launch_pp<256, 256, 2, 4, true>(p, 1, st) : launch_pp<256, 256, 2, 4, false>(p, 1, st);
     if (variant == 222) return one ? launch_pp<128, 128, 2, 2, true>(p, 2, st) : launch_pp<128, 128, 2, 2, false>(p, 2, st);
     if (variant == 223) return one ? launch_pp<256, 128, 4, 2, true>(p, 1, st) : launch_pp<256, 128, 4, 2, false>(p, 1, st);
+    // 8-phase persistent ring (conv_f16_p8_kernel)
+    if (variant == 231 && (one || p.cin % BKE == 0)) return launch_p8(p, one, st);
   }
   if (!det && p.cout > 32) {
     // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/
