@@ -23,7 +23,7 @@ DEV = 'cuda:0'
 
 CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15,
                  100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
-                 201, 202, 203, 204, 205, 206, 211, 212, 213, 214, 215, 216, 217, 221, 222, 223, 231]
+                 201, 202, 203, 204, 205, 206, 211, 212, 213, 214, 215, 216, 217, 221, 222, 223, 231, 232]
 DET_VARIANTS = [92, 97]
 
 

@@ -1217,10 +1217,12 @@ __global__ __launch_bounds__(64 * WM * WN, (2 * (BM + BN) * 128 <= 76 * 1024) ? 
 //    every wave computes its 64 x 32 part of the quadrant (16 MFMAs), reading A half ha (8
 //    ds_read_b128) and/or B half hb (4): phase 0 both, then B1, A1, B0 — so the halves' last reads
 //    fall in phases 0 (A0), 1 (B1), 2 (A1), 3 (B0).
-//  * a half is restaged two phases after its last read (the WAR distance with the stagger), so
-//    phase 0 stages A1 of k+1, phase 1 B0 of k+1, phase 2 A0 of k+2, phase 3 B1 of k+2; the only
-//    wait is phase 3's vmcnt(4): K-tile k+1 retired, k+2's first two halves still in flight, and
-//    the reads of k+1 start one phase (and so one more barrier of the other group) later.
+//  * every wave retires its phase's LDS reads (lgkmcnt(0)) before the phase's first barrier, so a
+//    half can be restaged ONE phase after its last read even with the groups staggered (the other
+//    group's DMA issue follows that barrier): phase 0 stages B0 of k+1, phase 1 A0 of k+2, phase 2
+//    B1 of k+2, phase 3 A1 of k+2; the only wait is phase 3's vmcnt(6): K-tile k+1 retired, three
+//    halves of k+2 still in flight, and the reads of k+1 start one phase (and so one more barrier of
+//    the other group) later.
 //  * the finished tile's epilogue (bias in the accumulators, activation, fp16, permlane16 pairing,
 //    16-byte NHWC stores) runs between the last K-tile's phase 3 and the next tile's phase 0.
 // acc[hb][j][ha][i] = channels hb*128 + wn*32 + j*16 + g*4 + e of pixel ha*128 + wm*64 + i*16 + li.
@@ -1229,7 +1231,6 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   constexpr int BM = 256, BN = 256, NTH = 512;
   constexpr int HALF = 128 * 128;                    // bytes per half-tile
   constexpr int BUF = 4 * HALF;                      // one K-tile: A0 A1 B0 B1
-  constexpr int NST = 16;                            // epilogue stores per lane per tile
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + 4096];
   float* bias_l = reinterpret_cast<float*>(smem + 2 * BUF);
 
@@ -1348,11 +1349,11 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     }
   };
 
-  // ---- prologue: K-tile 0 whole, K-tile 1's A0 and B1 in flight
+  // ---- prologue: K-tile 0 whole, K-tile 1's A0, B1 and A1 in flight
   stage_a(0); stage_b(1); stage_a(1); stage_b(0);
   if (total > 1) {
-    stage_a(0); stage_b(1);
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    stage_a(0); stage_b(1); stage_a(1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -1381,8 +1382,8 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       }
   };
   auto mfma_q = [&](int ha, int hb) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this phase's reads retired (WAR: see above)
     __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
@@ -1404,21 +1405,21 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     // phase 0: quadrant (0,0)
     read_b(bk + 2 * HALF);
     read_a(bk);
-    if (n1) stage_a(1);
+    if (n1) stage_b(0);
     mfma_q(0, 0);
     // phase 1: (0,1)
     read_b(bk + 3 * HALF);
-    if (n1) stage_b(0);
+    if (n2) stage_a(0);
     mfma_q(0, 1);
     // phase 2: (1,1)
     read_a(bk + HALF);
-    if (n2) stage_a(0);
+    if (n2) stage_b(1);
     mfma_q(1, 1);
-    // phase 3: (1,0); K-tile k+1 retired (k+2's A0 and B1 may stay in flight)
+    // phase 3: (1,0); K-tile k+1 retired (k+2's A0, B1 and A1 may stay in flight)
     read_b(bk + 2 * HALF);
     if (n2) {
-      stage_b(1);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      stage_a(1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1438,6 +1439,204 @@ hipError_t launch_p8_t(const ConvParams& p, int grid, hipStream_t st) {
   if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1>), dim3(grid), dim3(512), 0, st, p);
   else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 2>), dim3(grid), dim3(512), 0, st, p);
   else hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 0>), dim3(grid), dim3(512), 0, st, p);
+  return hipGetLastError();
+}
+
+// 8-phase-style persistent ring for 256 x 128 tiles (128-channel outputs, and 256-channel layers
+// with too few 256 x 256 tiles): 8 waves in two stagger groups as in conv_f16_p8_kernel, but with
+// three K-tile buffers of 48 KiB [A0 A1 B0 B1] (A halves 128 pixel rows, B halves 64 weight rows),
+// two phases per K-tile (phase h: A half h x the whole B tile, 16 MFMAs per wave on its 32 x 64
+// part), K-tile k+2 staged during K-tile k (A_h + B_h in phase h) into the buffer K-tile k-1 left,
+// and one counted vmcnt(6) per K-tile that retires K-tile k+1.
+// acc[h][j][i] = channels wn*64 + j*16 + g*4 + e of pixel h*128 + wm*32 + i*16 + li.
+template <bool ONE, int ACT>
+__global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p) {
+  constexpr int BM = 256, BN = 128, NTH = 512;
+  constexpr int AH = 128 * 128, BH = 64 * 128;
+  constexpr int BUF = 2 * AH + 2 * BH;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[3 * BUF + 4096];
+  float* bias_l = reinterpret_cast<float*>(smem + 3 * BUF);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int grp = wave >> 2;                         // stagger group (one wave of each per SIMD)
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g = lane >> 4, li = lane & 15;
+  const int lr = lane >> 3;
+  const int c = (lane & 7) ^ lr;
+
+  const int nN = (p.cout + BN - 1) / BN;
+  const int T = ((p.M + BM - 1) / BM) * nN;
+  const int G = gridDim.x;
+  const int nk = p.kpad / BKE;
+  const int ntl = (T - (int)blockIdx.x + G - 1) / G;
+  const int total = ntl * nk;
+
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto wr = make_rsrc(p.w, p.wbytes);
+  const auto yr = make_rsrc(p.y, 0x7fffffffu);
+  for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
+
+  // ---- staging cursor: K-tile s_gk, half h = A half h + B half h
+  int s_it = 0, s_kt = 0, s_gk = 0;
+  uint32_t a_off[2][2], b_off[2], a_so = 0;
+  KCursor<BKE> su;
+  auto stage = [&](int h) {
+    if (h == 0) {
+      if (s_kt == 0) {
+        const int t = blockIdx.x + s_it * G;
+        PixelWalk pw(p, (t / nN) * BM + wave * 8 + lr);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          if (q) pw.advance(p, 64);
+          a_off[q >> 1][q & 1] = a_origin(p, pw.b, pw.ho, pw.wo, c);
+        }
+        const int n0 = t % nN * BN;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) b_off[q] = (uint32_t)(((n0 + q * 64 + wave * 8 + lr) * p.kpad + c * 8) * 2);
+        su.init(p, 0);
+      }
+      a_so = ONE ? (uint32_t)s_kt * BKE * 2 : su.offset(p);
+      if (!ONE) su.advance(p);
+    }
+    unsigned char* d = smem + (s_gk % 3) * BUF;
+#pragma unroll
+    for (int j = 0; j < 2; ++j) dma16(xr, d + h * AH + (j * 8 + wave) * 8 * ROWB, a_off[h][j], a_so);
+    dma16(wr, d + 2 * AH + h * BH + wave * 8 * ROWB, b_off[h], (uint32_t)s_kt * BKE * 2);
+    if (h == 1) {
+      ++s_gk;
+      if (++s_kt == nk) { s_kt = 0; ++s_it; }
+    }
+  };
+
+  f4 acc[2][4][2];
+  int cm0 = 0, cn0 = 0;
+  auto init_tile = [&](int i) {
+    const int t = blockIdx.x + i * G;
+    cm0 = (t / nN) * BM;
+    cn0 = (t % nN) * BN;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int col = cn0 + wn * 64 + j * 16 + g * 4;
+      f4 bv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? bias_l[col + e] : 0.0f;
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) acc[h][j][i] = bv;
+    }
+  };
+  const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
+  auto epilogue = [&]() {
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      PixelWalk pw(p, cm0 + h * 128 + wm * 32 + li);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        if (i) pw.advance(p, 16);
+        const int m = cm0 + h * 128 + wm * 32 + i * 16 + li;
+        const uint32_t yo = (uint32_t)((pix_index(pw.b, pw.ho, pw.wo, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
+#pragma unroll
+        for (int mp = 0; mp < 2; ++mp) {
+          typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+          typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+          h4 va, vb;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            va[e] = (_Float16)act_t<ACT>(acc[h][2 * mp][i][e]);
+            vb[e] = (_Float16)act_t<ACT>(acc[h][2 * mp + 1][i][e]);
+          }
+          const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
+          const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+          const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+          const u4 v = {s0[0], s1[0], s0[1], s1[1]};
+          const int n = cn0 + wn * 64 + mp * 32 + (int)lane_ch;
+          const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
+          __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+        }
+      }
+    }
+  };
+
+  // ---- prologue: K-tiles 0 and 1 staged, 0 retired
+  stage(0); stage(1);
+  if (total > 1) {
+    stage(0); stage(1);
+    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  init_tile(0);
+  if (grp == 1) __builtin_amdgcn_s_barrier();
+
+  u4 xa[2][2], wb[2][4];
+  auto mfma_h = [&](int h) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+          acc[h][j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[sb][j]),
+                                                                __builtin_bit_cast(h8, xa[sb][i]), acc[h][j][i], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  };
+  auto read_a = [&](const unsigned char* ah) {
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const int row = wm * 32 + i * 16 + li;
+        xa[sb][i] = *reinterpret_cast<const u4*>(ah + row * ROWB + swz(row, sb * 4 + g) * 16);
+      }
+  };
+
+  int ci = 0, ckt = 0;
+  for (int k = 0; k < total; ++k) {
+    const unsigned char* bk = smem + (k % 3) * BUF;
+    const bool n2 = k + 2 < total;
+    // phase 0: the wave's whole B part (kept for phase 1) + A half 0
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int row = j * 16 + li;   // within B half wn
+        wb[sb][j] = *reinterpret_cast<const u4*>(bk + 2 * AH + wn * BH + row * ROWB + swz(row, sb * 4 + g) * 16);
+      }
+    read_a(bk);
+    if (n2) stage(0);
+    mfma_h(0);
+    // phase 1: A half 1; K-tile k+1 retired (k+2 may stay in flight)
+    read_a(bk + AH);
+    if (n2) {
+      stage(1);
+      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    mfma_h(1);
+    if (++ckt == nk) {
+      epilogue();
+      ckt = 0;
+      if (++ci < ntl) init_tile(ci);
+    }
+  }
+  if (grp == 0) __builtin_amdgcn_s_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool ONE>
+hipError_t launch_p8n_t(const ConvParams& p, int grid, hipStream_t st) {
+  if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8n_kernel<ONE, 1>), dim3(grid), dim3(512), 0, st, p);
+  else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8n_kernel<ONE, 2>), dim3(grid), dim3(512), 0, st, p);
+  else hipLaunchKernelGGL((conv_f16_p8n_kernel<ONE, 0>), dim3(grid), dim3(512), 0, st, p);
   return hipGetLastError();
 }
 
@@ -1469,6 +1668,13 @@ hipError_t launch_p8(const ConvParams& p, bool one, hipStream_t st) {
   const long T = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
   const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
   return one ? launch_p8_t<true>(p, grid, st) : launch_p8_t<false>(p, grid, st);
+}
+
+hipError_t launch_p8n(const ConvParams& p, bool one, hipStream_t st) {
+  if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || (!one && p.cin % BKE)) return hipErrorInvalidValue;
+  const long T = (long)((p.M + 255) / 256) * ((p.cout + 127) / 128);
+  const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
+  return one ? launch_p8n_t<true>(p, grid, st) : launch_p8n_t<false>(p, grid, st);
 }
 
 template <int BM, int BN, int WM, int WN, bool ONE>
@@ -1641,6 +1847,15 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // @80 90 -> 77, 256->512 @40 157 -> 134, 512->1024 @20 146 -> 128.  Under 200 tiles (@20 with
     // cout <= 512) the persistent 256 x 256 ring loses (2048->512 @20 41 -> 59).  YV7_WIDE_PRING=0: off.
     static const int wide = [] { const char* e = getenv("YV7_WIDE_PRING"); return e ? atoi(e) : 1; }();
+    // The 8-phase ring (conv_f16_p8_kernel) where it measured faster in-network (scripts/tune_ops.py,
+    // one layer forced at a time, bs 32, us, dispatch before -> p8): 3x3 256->256 @40 76 -> 67, s2
+    // 256->256 @80 79 -> 72, 256->512 @40 137 -> 126, 512->1024 @20 130 -> 114; 1x1 with K >= 1024:
+    // 1024->1024 @40 142 -> 138, 1024->512 @40 74 -> 70, 1024->256 @40 41 -> 39.  Short-K 1x1 and
+    // 128-input 3x3 layers stay on the 2-phase ring (1x1 256->256 @160 199 -> 216, 3x3 128->256 @80
+    // 137 -> 144).  YV7_P8=0: off.
+    static const int p8 = [] { const char* e = getenv("YV7_P8"); return e ? atoi(e) : 1; }();
+    if (p8 && t256 >= 200 && p.cout >= 256 && ((one && p.K >= 1024) || (p.k == 3 && p.cin >= 256 && p.cin % BKE == 0)))
+      return launch_p8(p, one, st);
     if (one) {
       if (p.K >= 256 && p.cout >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
       if (wide && p.cout >= 256 && t256 >= 200) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
@@ -1679,6 +1894,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 223) return one ? launch_pp<256, 128, 4, 2, true>(p, 1, st) : launch_pp<256, 128, 4, 2, false>(p, 1, st);
     // 8-phase persistent ring (conv_f16_p8_kernel)
     if (variant == 231 && (one || p.cin % BKE == 0)) return launch_p8(p, one, st);
+    if (variant == 232 && (one || p.cin % BKE == 0)) return launch_p8n(p, one, st);
   }
   if (!det && p.cout > 32) {
     // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/
