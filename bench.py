@@ -32,7 +32,9 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # HBM bytes per conv launch from PMC counters of this same workload (scripts/pmc_traffic.sh: separate
 # FETCH_SIZE / WRITE_SIZE rocprofv3 passes; scripts/pmc_traffic.py: x2 FETCH correction for gfx950)
-PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r1_pmc_traffic.json')
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r2_pmc_traffic.json')
+if not os.path.exists(PMC_TRAFFIC):
+    PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r1_pmc_traffic.json')
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA
 
 
@@ -465,7 +467,7 @@ def main(argv=None):
                        'weights': 'seeded synthetic, RCCL-broadcast' if distributed else 'seeded synthetic'},
             'roofline': {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
                          'frac': round(achieved_gbs / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                         'traffic_unit': 'bytes per launch (PMC, profiles/r1_pmc_traffic.json)',
+                         'traffic_unit': f'bytes per launch (PMC, profiles/{os.path.basename(PMC_TRAFFIC)})',
                          'kernel': 'conv kernels (MFMA implicit-GEMM ring / persistent ring / weight-stationary '
                                    '3x3 / halo; all CONV and DETECT launches of the forward)',
                          'launches_per_forward': nconv, 'mean_launch_us': round(mean_launch_s * 1e6, 2),

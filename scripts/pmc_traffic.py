@@ -5,7 +5,7 @@ wide streaming read, so read bytes = 2 x FETCH_SIZE; WRITE_SIZE is exact for 16-
 rocprofv3 reports both in KiB.  Output: profiles/<name>.json with, per kernel family, the launches
 and the corrected mean bytes per launch, plus the conv family (CONV / DETECT launches) that bench.py
 reports as roofline.traffic.
-usage: python scripts/pmc_traffic.py gpurun_out profiles/r1_pmc_traffic.json
+usage: python scripts/pmc_traffic.py gpurun_out profiles/r2_pmc_traffic.json
 """
 import collections
 import csv
@@ -26,6 +26,7 @@ def load(d, counter):
 
 def family(name):
     for k in ('conv3x3_halo_kernel', 'conv3x3_ws64_kernel', 'conv_f16_pring_kernel', 'conv_f16_ring_kernel',
+              'conv_f16_p8n_kernel', 'conv_f16_p8_kernel', 'conv_f16_pp_kernel', 'conv_f8_kernel',
               'conv_f16_kernel', 'conv_kernel', 'stem_kernel', 'spp_cascade_kernel', 'maxpool_kernel',
               'upsample_kernel', 'copy_kernel', 'input_reorg16_kernel', 'input_kernel', 'letterbox_kernel', 'nms_'):
         if k in name:
@@ -47,6 +48,7 @@ def main(src, dst):
         res['families'][f] = {'launches': n, 'read_bytes_per_launch': rb / n, 'write_bytes_per_launch': wb / n,
                               'hbm_bytes_per_launch': (rb + wb) / n}
         if f in ('conv3x3_halo_kernel', 'conv3x3_ws64_kernel', 'conv_f16_pring_kernel', 'conv_f16_ring_kernel',
+                 'conv_f16_p8n_kernel', 'conv_f16_p8_kernel', 'conv_f16_pp_kernel', 'conv_f8_kernel',
                  'conv_f16_kernel', 'conv_kernel'):
             conv_n += n
             conv_b += rb + wb

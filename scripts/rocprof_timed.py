@@ -13,7 +13,7 @@ import statistics
 import sys
 
 CONV = ('conv_f16_pring_kernel', 'conv_f16_ring_kernel', 'conv3x3_ws64_kernel', 'conv3x3_halo_kernel',
-        'conv_f16_kernel', 'conv_f16_pp_kernel', 'conv_f8_kernel')
+        'conv_f16_kernel', 'conv_f16_pp_kernel', 'conv_f16_p8_kernel', 'conv_f16_p8n_kernel', 'conv_f8_kernel')
 NMS = ('nms_compact', 'nms_fast', 'nms_rows', 'nms_scan', 'nms_write', 'nms_sort', 'nms_greedy')
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Dispatch_Id']))
