@@ -862,9 +862,10 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
 
   const int nN = (p.cout + BN - 1) / BN;
   const int T = ((p.M + BM - 1) / BM) * nN;
-  const int G = gridDim.x;
   const int nk = p.kpad / BK;
-  const int ntl = (T - (int)blockIdx.x + G - 1) / G;
+  const TileWalk tw = xcd_tile_walk(T);   // XCD-major persistent tile order
+  const int ntl = tw.count();
+  if (ntl == 0) return;
   const int nsteps = ntl * nk;
 
   const auto xr = make_rsrc(p.x, p.xbytes);
@@ -879,7 +880,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
   int ig = 0, it = 0, ikt = 0;
   auto issue_next = [&]() {
     if (ikt == 0) {
-      const int t = blockIdx.x + it * G;
+      const int t = tw.at(it);
       const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
       aw.init(p, c, 0);
       PixelWalk pw(p, m0 + wave * RPI + lr);
@@ -907,7 +908,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
   f4 acc[TN][TM];
   int cm0 = 0, cn0 = 0;
   auto init_tile = [&](int i) {
-    const int t = blockIdx.x + i * G;
+    const int t = tw.at(i);
     cm0 = (t / nN) * BM;
     cn0 = (t % nN) * BN;
 #pragma unroll
@@ -1226,7 +1227,9 @@ __global__ __launch_bounds__(64 * WM * WN, (2 * (BM + BN) * 128 <= 76 * 1024) ? 
 //  * the finished tile's epilogue (bias in the accumulators, activation, fp16, permlane16 pairing,
 //    16-byte NHWC stores) runs between the last K-tile's phase 3 and the next tile's phase 0.
 // acc[hb][j][ha][i] = channels hb*128 + wn*32 + j*16 + g*4 + e of pixel ha*128 + wm*64 + i*16 + li.
-template <bool ONE, int ACT>
+// OPT (experiments, variants 240 + OPT): 1 = DMA issued before the phase's LDS reads, 2 = no s_setprio,
+// 4 = XCD-major persistent tile order, 8 = only group 1 retires its reads before the first barrier
+template <bool ONE, int ACT, int OPT = 0>
 __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p) {
   constexpr int BM = 256, BN = 256, NTH = 512;
   constexpr int HALF = 128 * 128;                    // bytes per half-tile
@@ -1245,7 +1248,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   const int T = ((p.M + BM - 1) / BM) * nN;
   const int G = gridDim.x;
   const int nk = p.kpad / BKE;
-  const int ntl = (T - (int)blockIdx.x + G - 1) / G;
+  // persistent tile order: XCD-major (OPT 4, xcd_tile_walk), else tiles blockIdx, + G, ...
+  const TileWalk tw = (OPT & 4) ? xcd_tile_walk(T) : TileWalk{(int)blockIdx.x, G, T};
+  const int ntl = tw.count();
+  if (ntl == 0) return;
   const int total = ntl * nk;                        // K-tiles this block computes
 
   const auto xr = make_rsrc(p.x, p.xbytes);
@@ -1260,7 +1266,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   auto stage_a = [&](int h) {   // half h (0 / 1) of K-tile a_gk
     if (h == 0) {
       if (a_kt == 0) {
-        const int t = blockIdx.x + a_it * G;
+        const int t = tw.at(a_it);
         PixelWalk pw(p, (t / nN) * BM + wave * 8 + lr);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1282,7 +1288,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   };
   auto stage_b = [&](int h) {   // half h of K-tile b_gk; staged B1 first, then B0
     if (h == 1 && b_kt == 0) {
-      const int n0 = (blockIdx.x + b_it * G) % nN * BN;
+      const int n0 = tw.at(b_it) % nN * BN;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         b_off[q >> 1][q & 1] = (uint32_t)(((n0 + (q >> 1) * 128 + ((q & 1) * 8 + wave) * 8 + lr) * p.kpad + c * 8) * 2);
@@ -1300,7 +1306,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   f4 acc[2][2][2][4];
   int cm0 = 0, cn0 = 0;
   auto init_tile = [&](int i) {
-    const int t = blockIdx.x + i * G;
+    const int t = tw.at(i);
     cm0 = (t / nN) * BM;
     cn0 = (t % nN) * BN;
 #pragma unroll
@@ -1382,9 +1388,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       }
   };
   auto mfma_q = [&](int ha, int hb) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this phase's reads retired (WAR: see above)
+    if (!(OPT & 8) || wm == 1)
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this phase's reads retired (WAR: see above)
     __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
+    if (!(OPT & 2)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
@@ -1394,7 +1401,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
           acc[hb][j][ha][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[sb][j]),
                                                                      __builtin_bit_cast(h8, xa[sb][i]),
                                                                      acc[hb][j][ha][i], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
+    if (!(OPT & 2)) __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
 
@@ -1402,23 +1409,28 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   for (int k = 0; k < total; ++k) {
     const unsigned char* bk = smem + (k & 1) * BUF;
     const bool n1 = k + 1 < total, n2 = k + 2 < total;
+    constexpr bool DF = (OPT & 1) != 0;   // DMA first
     // phase 0: quadrant (0,0)
+    if (DF && n1) stage_b(0);
     read_b(bk + 2 * HALF);
     read_a(bk);
-    if (n1) stage_b(0);
+    if (!DF && n1) stage_b(0);
     mfma_q(0, 0);
     // phase 1: (0,1)
+    if (DF && n2) stage_a(0);
     read_b(bk + 3 * HALF);
-    if (n2) stage_a(0);
+    if (!DF && n2) stage_a(0);
     mfma_q(0, 1);
     // phase 2: (1,1)
+    if (DF && n2) stage_b(1);
     read_a(bk + HALF);
-    if (n2) stage_b(1);
+    if (!DF && n2) stage_b(1);
     mfma_q(1, 1);
     // phase 3: (1,0); K-tile k+1 retired (k+2's A0, B1 and A1 may stay in flight)
+    if (DF && n2) stage_a(1);
     read_b(bk + 2 * HALF);
     if (n2) {
-      stage_a(1);
+      if (!DF) stage_a(1);
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1436,9 +1448,20 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
 
 template <bool ONE>
 hipError_t launch_p8_t(const ConvParams& p, int grid, hipStream_t st) {
-  if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1>), dim3(grid), dim3(512), 0, st, p);
-  else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 2>), dim3(grid), dim3(512), 0, st, p);
-  else hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 0>), dim3(grid), dim3(512), 0, st, p);
+  if (p.act == 1 && p.variant >= 241 && p.variant <= 255) {   // experiments (SiLU layers only; 244 = 231)
+    switch (p.variant - 240) {
+      case 15: hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, 0>), dim3(grid), dim3(512), 0, st, p); return hipGetLastError();
+#define P8X(o) case o: hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, o>), dim3(grid), dim3(512), 0, st, p); return hipGetLastError();
+      P8X(1) P8X(2) P8X(8) P8X(5) P8X(12) P8X(13)
+      case 4: break;   // the default
+#undef P8X
+      default: break;
+    }
+  }
+  // XCD-major tile order (OPT 4): 1x1 1024->1024 @40 140 -> 133 us, 3x3 layers unchanged (tune_ops)
+  if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, 4>), dim3(grid), dim3(512), 0, st, p);
+  else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 2, 4>), dim3(grid), dim3(512), 0, st, p);
+  else hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 0, 4>), dim3(grid), dim3(512), 0, st, p);
   return hipGetLastError();
 }
 
@@ -1893,7 +1916,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 222) return one ? launch_pp<128, 128, 2, 2, true>(p, 2, st) : launch_pp<128, 128, 2, 2, false>(p, 2, st);
     if (variant == 223) return one ? launch_pp<256, 128, 4, 2, true>(p, 1, st) : launch_pp<256, 128, 4, 2, false>(p, 1, st);
     // 8-phase persistent ring (conv_f16_p8_kernel)
-    if (variant == 231 && (one || p.cin % BKE == 0)) return launch_p8(p, one, st);
+    if ((variant == 231 || (variant > 240 && variant < 256)) && (one || p.cin % BKE == 0)) return launch_p8(p, one, st);
     if (variant == 232 && (one || p.cin % BKE == 0)) return launch_p8n(p, one, st);
   }
   if (!det && p.cout > 32) {

@@ -60,7 +60,6 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
   const int tx_n = p.W / TS, tpi = tx_n * (p.H / TS), T = p.B * tpi;
-  const int G = gridDim.x;
 
   const auto xr = make_rsrc(p.x, p.xbytes);
   const auto yr = make_rsrc(p.y, 0x7fffffffu);
@@ -208,8 +207,12 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
   //   wait for patch(t) (the only older memory op besides the previous tile's epilogue stores, which
   //   are younger) -> barrier (also: every wave finished reading buffer b^1) -> DMA patch(t+G) into
   //   b^1 -> tile t's MFMAs with the previous tile's epilogue interleaved.
-  int t = blockIdx.x;
-  if (t >= T) return;
+  // XCD-major persistent tile walk (xcd_tile_walk): the blocks of one XCD take neighbouring tiles, so
+  // the halo rows two adjacent tiles share come from that XCD's L2
+  const TileWalk tw = xcd_tile_walk(T);
+  int t = tw.t;
+  const int TS_ = tw.step, TE = tw.end;
+  if (t >= TE) return;
   issue_patch(t, 0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // weight ds_writes of this wave
   f4 accA[4][4], accB[4][4];
@@ -218,26 +221,26 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
   // first tile: no epilogue to interleave
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
-  if (t + G < T) issue_patch(t + G, 1);
+  if (t + TS_ < TE) issue_patch(t + TS_, 1);
   init_acc(accA);
   tile_mfma(smem, accA, [](int) {});
   oprev = out_origin(t);
-  t += G;
+  t += TS_;
   buf = 1;
   // steady state, two tiles per trip so the accumulator sets swap roles without copies
   bool stores_out = false;   // the previous iteration issued an epilogue (NSTORE younger stores)
-  while (t < T) {
+  while (t < TE) {
     if (stores_out) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stores_out = true;
     if (p.variant != 16) __builtin_amdgcn_s_barrier();
-    if (t + G < T) issue_patch(t + G, buf ^ 1);
+    if (t + TS_ < TE) issue_patch(t + TS_, buf ^ 1);
     init_acc(accB);
     tile_mfma(smem + buf * PBUF, accB, [&](int ss) { if (p.variant != 14 && p.variant != 16) for (int q = (ss * 4) / 3; q < ((ss + 1) * 4) / 3; ++q) epi_piece(accA, oprev, q); });
     oprev = out_origin(t);
-    t += G;
+    t += TS_;
     buf ^= 1;
-    if (t >= T) {
+    if (t >= TE) {
 #pragma unroll
       for (int q = 0; q < 8; ++q) epi_piece(accB, oprev, q);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -245,11 +248,11 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     }
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
     if (p.variant != 16) __builtin_amdgcn_s_barrier();
-    if (t + G < T) issue_patch(t + G, buf ^ 1);
+    if (t + TS_ < TE) issue_patch(t + TS_, buf ^ 1);
     init_acc(accA);
     tile_mfma(smem + buf * PBUF, accA, [&](int ss) { if (p.variant != 14 && p.variant != 16) for (int q = (ss * 4) / 3; q < ((ss + 1) * 4) / 3; ++q) epi_piece(accB, oprev, q); });
     oprev = out_origin(t);
-    t += G;
+    t += TS_;
     buf ^= 1;
   }
 #pragma unroll

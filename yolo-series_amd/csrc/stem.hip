@@ -150,13 +150,19 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   for (int nt = 0; nt < NAT; ++nt)
 #pragma unroll
     for (int e = 0; e < 4; ++e) ba_l[nt][e] = p.ba[nt * 16 + g * 4 + e] * sa_scale;
-  if ((int)blockIdx.x < ntiles) prefetch(blockIdx.x);
-  for (int tile = blockIdx.x; tile < ntiles; tile += gridDim.x) {
+  // XCD-major tile order: the blocks of one XCD (blockIdx % 8 on the round-robin dispatch) walk
+  // consecutive tiles, so the image lines two horizontally / vertically adjacent tiles share are
+  // fetched into that XCD's L2 once (row-order assignment spread neighbours over all 8 L2s: 4.5x
+  // the image's bytes read from HBM)
+  const int G = gridDim.x;
+  const int vb = G % 8 == 0 ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (vb < ntiles) prefetch(vb);
+  for (int tile = vb; tile < ntiles; tile += G) {
   tile_geom(tile, b, oy0, ox0);
   ay0 = 2 * oy0 - 1;
   ax0 = 2 * ox0 - 1;
   commit();
-  if (tile + (int)gridDim.x < ntiles) prefetch(tile + gridDim.x);
+  if (tile + G < ntiles) prefetch(tile + G);
   __syncthreads();
 
   // 2. conv A on MFMA -> abuf

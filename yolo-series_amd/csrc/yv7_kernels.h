@@ -16,6 +16,23 @@ template <typename T> struct Vec;
 template <> struct Vec<_Float16> { static constexpr int N = 8; };
 template <> struct Vec<float> { static constexpr int N = 4; };
 
+// Persistent tile walk, XCD-major: the 8 XCDs (blockIdx % 8 on the round-robin dispatch) each take a
+// contiguous eighth of the T tiles, walked by that XCD's blocks (t, t + step, ... < end), so
+// neighbouring tiles — sharing halo rows / operand panels — are fetched into one L2, and a partial
+// last round is spread evenly over the XCDs.  Falls back to t = blockIdx, step = gridDim when the grid
+// is not a multiple of 8.
+struct TileWalk {
+  int t, step, end;
+  __device__ __forceinline__ int count() const { return t < end ? (end - t + step - 1) / step : 0; }
+  __device__ __forceinline__ int at(int i) const { return t + i * step; }
+};
+__device__ __forceinline__ TileWalk xcd_tile_walk(int T) {
+  const int G = gridDim.x, b = blockIdx.x;
+  if (G % 8) return TileWalk{b, G, T};
+  const int x = b % 8, gx = G / 8;
+  return TileWalk{(int)((long)x * T / 8) + b / 8, gx, (int)((long)(x + 1) * T / 8)};
+}
+
 template <int ACT>
 __device__ __forceinline__ float act_t(float v) {
   // SiLU with v_exp_f32 / v_rcp_f32 (~1 ulp each): plenty for an fp16 output, ~4x cheaper than the
