@@ -338,7 +338,8 @@ __device__ __forceinline__ void det_tail(const ConvParams& p, unsigned char* sme
         rec[1] = best;
         rec[2] = __builtin_bit_cast(float, bc);
         rec[3] = 0.0f;
-        *reinterpret_cast<f4*>(p.best + (size_t)(t.zrow0[pr] + (long long)a * hw) * 4) = rec;
+        // z and the row records are streamed out (non-temporal): nothing re-reads them before the NMS
+        __builtin_nontemporal_store(rec, reinterpret_cast<f4*>(p.best + (size_t)(t.zrow0[pr] + (long long)a * hw) * 4));
       }
     }
   }
@@ -357,13 +358,13 @@ __device__ __forceinline__ void det_tail(const ConvParams& p, unsigned char* sme
       const long long z0 = t.zrow0[grp * 4];
       const f4 v = reinterpret_cast<const f4*>(zs + (a * BM + grp * 4) * NO)[c];
       if (z0 >= 0 && t.zrow0[grp * 4 + 3] == z0 + 3 && ((z0 + aoff) & 3) == 0) {
-        reinterpret_cast<f4*>(p.z + (size_t)(z0 + aoff) * NO)[c] = v;
+        __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p.z + (size_t)(z0 + aoff) * NO) + c);
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
           const int e = 4 * c + k, rk = e / NO, ok = e - rk * NO;
           const long long zr = t.zrow0[grp * 4 + rk];
-          if (zr >= 0) p.z[(size_t)(zr + aoff) * NO + ok] = v[k];
+          if (zr >= 0) __builtin_nontemporal_store(v[k], p.z + (size_t)(zr + aoff) * NO + ok);
         }
       }
     }
@@ -946,7 +947,8 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
         const int n = cn0 + wn * WTN + mp * 32 + (int)lane_ch;
         // rows past M / channels past cout: an offset beyond the buffer drops the store
         const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
-        __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+        if (p.store_nt) __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 2);
+        else __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
       }
     }
   };
@@ -1349,7 +1351,8 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
           const u4 v = {s0[0], s1[0], s0[1], s1[1]};
           const int n = cn0 + hb * 128 + wn * 32 + (int)lane_ch;
           const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
-          __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+          if (p.store_nt) __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 2);
+          else __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
         }
       }
     }
