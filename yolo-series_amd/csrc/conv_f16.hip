@@ -958,8 +958,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
         const int n = cn0 + wn * WTN + mp * 32 + (int)lane_ch;
         // rows past M / channels past cout: an offset beyond the buffer drops the store
         const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
-        if (p.store_nt) __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 2);
-        else __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
       }
     }
   };
@@ -1362,8 +1361,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
           const u4 v = {s0[0], s1[0], s0[1], s1[1]};
           const int n = cn0 + hb * 128 + wn * 32 + (int)lane_ch;
           const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
-          if (p.store_nt) __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 2);
-          else __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
+          __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
         }
       }
     }

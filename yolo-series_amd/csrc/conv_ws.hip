@@ -193,10 +193,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
     const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
     const u4 v = {s0[0], s1[0], s0[1], s1[1]};
-    if (p.variant != 12) {
-      if (p.store_nt) __builtin_amdgcn_raw_buffer_store_b128(v, yr, o0 + i * rowb + m * 64 + lane_ch, 0, 2);
-      else __builtin_amdgcn_raw_buffer_store_b128(v, yr, o0 + i * rowb + m * 64 + lane_ch, 0, 0);
-    }
+    if (p.variant != 12)
+      __builtin_amdgcn_raw_buffer_store_b128(v, yr, o0 + i * rowb + m * 64 + lane_ch, 0, 0);
   };
   auto init_acc = [&](f4 (&acc)[4][4]) {
 #pragma unroll

@@ -117,8 +117,6 @@ yv7::ConvParams conv_params(const yv7_plan* p, size_t op, int B, int H, int W) {
   const size_t es = elem_size(p->dtype);
   yv7::ConvParams c;
   std::memset(&c, 0, sizeof(c));
-  static const int store_nt = [] { const char* e = getenv("YV7_STORE_NT"); return e ? atoi(e) : 0; }();
-  c.store_nt = store_nt;
   c.B = B;
   c.H = H >> ti.shift;
   c.W = W >> ti.shift;

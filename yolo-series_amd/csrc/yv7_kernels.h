@@ -96,7 +96,6 @@ struct ConvParams {
   int cnt_n;
   int ksplit;
   int pool;           // 2: 1x1 conv over the 2x2 / stride-2 max of the input (MP folded in; k = 1, s = 2)
-  int store_nt;       // experiment (YV7_STORE_NT): non-temporal output stores in the persistent kernels
 };
 
 // Split-K scratch the fp16 dispatch needs for one conv (0 when it does not split).
