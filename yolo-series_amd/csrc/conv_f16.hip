@@ -1298,8 +1298,9 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       if (++a_kt == nk) { a_kt = 0; ++a_it; }
     }
   };
-  auto stage_b = [&](int h) {   // half h of K-tile b_gk; staged B1 first, then B0
-    if (h == 1 && b_kt == 0) {
+  constexpr int BFIRST = (OPT & 16) ? 0 : 1;   // which B half of a K-tile is staged first
+  auto stage_b = [&](int h) {   // half h of K-tile b_gk; staged B1 first, then B0 (OPT 16: B0, then B1)
+    if (h == BFIRST && b_kt == 0) {
       const int n0 = tw.at(b_it) % nN * BN;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
@@ -1308,7 +1309,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     unsigned char* d = smem + (b_gk & 1) * BUF + (2 + h) * HALF;
 #pragma unroll
     for (int j = 0; j < 2; ++j) dma16(wr, d + (j * 8 + wave) * 8 * ROWB, b_off[h][j], (uint32_t)b_kt * BKE * 2);
-    if (h == 0) {
+    if (h != BFIRST) {
       ++b_gk;
       if (++b_kt == nk) { b_kt = 0; ++b_it; }
     }
@@ -1367,7 +1368,16 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     }
   };
 
-  // ---- prologue: K-tile 0 whole, K-tile 1's A0, B1 and A1 in flight
+  // ---- prologue: K-tile 0 whole, K-tile 1's A0, B1 and A1 in flight (OPT 16: all of K-tile 1)
+  if constexpr ((OPT & 16) != 0) {
+    stage_a(0); stage_b(0); stage_b(1); stage_a(1);
+    if (total > 1) {
+      stage_a(0); stage_b(0); stage_b(1); stage_a(1);
+      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+  } else {
   stage_a(0); stage_b(1); stage_a(1); stage_b(0);
   if (total > 1) {
     stage_a(0); stage_b(1); stage_a(1);
@@ -1375,12 +1385,13 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
+  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bias_l
   __builtin_amdgcn_s_barrier();
   init_tile(0);
   if (wm == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind group 0
 
-  u4 xa[2][4], wb[2][2];
+  u4 xa[2][4], wb[2][2], wb1[2][2];   // wb1: OPT 16 keeps B half 1's fragments apart from half 0's
   auto read_a = [&](const unsigned char* h) {
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
@@ -1390,14 +1401,31 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
         xa[sb][i] = *reinterpret_cast<const u4*>(h + row * ROWB + swz(row, sb * 4 + g) * 16);
       }
   };
-  auto read_b = [&](const unsigned char* h) {
+  auto read_b_to = [&](const unsigned char* h, u4 (&w)[2][2]) {
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int row = wn * 32 + j * 16 + li;
-        wb[sb][j] = *reinterpret_cast<const u4*>(h + row * ROWB + swz(row, sb * 4 + g) * 16);
+        w[sb][j] = *reinterpret_cast<const u4*>(h + row * ROWB + swz(row, sb * 4 + g) * 16);
       }
+  };
+  auto read_b = [&](const unsigned char* h) { read_b_to(h, wb); };
+  auto mfma_qw = [&](int ha, int hb, const u4 (&w)[2][2]) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+          acc[hb][j][ha][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w[sb][j]),
+                                                                     __builtin_bit_cast(h8, xa[sb][i]),
+                                                                     acc[hb][j][ha][i], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
   };
   auto mfma_q = [&](int ha, int hb) {
     if (!(OPT & 8) || wm == 1)
@@ -1418,6 +1446,45 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   };
 
   int ci = 0, ckt = 0;
+  if constexpr ((OPT & 16) != 0) {
+    // OPT 16: B half 0's fragments stay in registers from phase 0 to phase 3, so A0 and B0 are both
+    // free after phase 0: K-tile k+2 is staged whole in phases 1-3 (A0+B0, B1, A1) and the tile
+    // epilogue's stores, issued after phase 3, are younger than every load a later wait retires —
+    // phase 3 waits with vmcnt(8 [+ 16 while the previous tile's stores are in flight])
+    bool st = false;   // the epilogue after K-tile k-1 issued its stores
+    for (int k = 0; k < total; ++k) {
+      const unsigned char* bk = smem + (k & 1) * BUF;
+      const bool n2 = k + 2 < total;
+      read_b_to(bk + 2 * HALF, wb);
+      read_a(bk);
+      mfma_qw(0, 0, wb);
+      read_b_to(bk + 3 * HALF, wb1);
+      if (n2) { stage_a(0); stage_b(0); }
+      mfma_qw(0, 1, wb1);
+      read_a(bk + HALF);
+      if (n2) stage_b(1);
+      mfma_qw(1, 1, wb1);
+      if (n2) stage_a(1);
+      if (n2) {
+        if (st) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        if (st) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      st = false;
+      mfma_qw(1, 0, wb);
+      if (++ckt == nk) {
+        epilogue();
+        st = true;
+        ckt = 0;
+        if (++ci < ntl) init_tile(ci);
+      }
+    }
+    if (wm == 0) __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    return;
+  }
   for (int k = 0; k < total; ++k) {
     const unsigned char* bk = smem + (k & 1) * BUF;
     const bool n1 = k + 1 < total, n2 = k + 2 < total;
@@ -1460,6 +1527,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
 
 template <bool ONE>
 hipError_t launch_p8_t(const ConvParams& p, int grid, hipStream_t st) {
+  if (p.act == 1 && p.variant == 233) {   // experiment: OPT 16 schedule (+ XCD order)
+    hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, 20>), dim3(grid), dim3(512), 0, st, p);
+    return hipGetLastError();
+  }
   if (p.act == 1 && p.variant >= 241 && p.variant <= 255) {   // experiments (SiLU layers only; 244 = 231)
     switch (p.variant - 240) {
       case 15: hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, 0>), dim3(grid), dim3(512), 0, st, p); return hipGetLastError();
@@ -1928,7 +1999,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 222) return one ? launch_pp<128, 128, 2, 2, true>(p, 2, st) : launch_pp<128, 128, 2, 2, false>(p, 2, st);
     if (variant == 223) return one ? launch_pp<256, 128, 4, 2, true>(p, 1, st) : launch_pp<256, 128, 4, 2, false>(p, 1, st);
     // 8-phase persistent ring (conv_f16_p8_kernel)
-    if ((variant == 231 || (variant > 240 && variant < 256)) && (one || p.cin % BKE == 0)) return launch_p8(p, one, st);
+    if ((variant == 231 || variant == 233 || (variant > 240 && variant < 256)) && (one || p.cin % BKE == 0)) return launch_p8(p, one, st);
     if (variant == 232 && (one || p.cin % BKE == 0)) return launch_p8n(p, one, st);
   }
   if (!det && p.cout > 32) {
