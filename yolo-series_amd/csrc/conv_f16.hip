@@ -834,7 +834,10 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
 //    LDS staging;
 //  * counted vmcnt waits: the loads younger than the awaited stage are the next stages and, right
 //    after a tile boundary, the previous tile's stores (their number is known per step).
-template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int ACT, int BK>
+// WS > 0: weight-stationary 1x1 form — the layer's whole weight matrix (cout <= BN, K <= WS steps)
+// is DMA'd into LDS once per block and every tile's K steps read it from there, so only the
+// activation tile streams (a third of the DMA issue of the 256 x 256 ring); bias in registers.
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int ACT, int BK, int WS = 0>
 __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 1024) ? 2 : 1) void conv_f16_pring_kernel(
     const ConvParams p) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
@@ -847,12 +850,15 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
   static_assert(RA * RPI * NW == BM && RB * RPI * NW == BN, "tile rows must split into DMA groups per wave");
   static_assert(TN % 2 == 0, "the epilogue pairs 16-channel groups");
   static_assert(STAGES >= 2 && STAGES <= 4, "counted waits cover up to two stages in flight");
-  constexpr int PER = RA + RB;
+  static_assert(WS == 0 || ONE, "weight-stationary form: 1x1 convs only");
+  constexpr int PER = RA + (WS ? 0 : RB);
   constexpr int NST = TM * TN / 2;   // epilogue stores per lane per tile
-  constexpr int STAGE = (BM + BN) * RB_;
-  constexpr int BIAS = 4096;         // bias vector (<= 1024 channels) behind the ring
-  __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + BIAS];
-  float* bias_l = reinterpret_cast<float*>(smem + STAGES * STAGE);
+  constexpr int STAGE = (BM + (WS ? 0 : BN)) * RB_;
+  constexpr int WREG = WS ? BN * WS * RB_ : 0;   // stationary weights: [K step][BN rows][RB_]
+  constexpr int BIAS = WS ? 0 : 4096;            // bias vector (<= 1024 channels) behind the ring
+  __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + WREG + BIAS];
+  float* bias_l = reinterpret_cast<float*>(smem + STAGES * STAGE + WREG);
+  unsigned char* wl = smem + STAGES * STAGE;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -873,7 +879,25 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
   const auto wr = make_rsrc(p.w, p.wbytes);
   const auto yr = make_rsrc(p.y, 0x7fffffffu);
 
-  for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
+  float bias_r[WS ? TN : 1][4];
+  if constexpr (WS == 0) {
+    for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
+  } else {
+    // (one N tile: cn0 = 0) this lane's channels, and the layer's weights into LDS once
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int col = wn * WTN + j * 16 + g * 4 + e;
+        bias_r[j][e] = col < p.cout ? p.bias[col] : 0.0f;
+      }
+    constexpr int GPS = BN / RPI;   // DMA groups per K step
+    for (int q = wave; q < nk * GPS; q += NW) {
+      const int ks = q / GPS, rg = q - ks * GPS;
+      dma16(wr, wl + (ks * BN + rg * RPI) * RB_, (uint32_t)(((rg * RPI + lr) * p.kpad + c * 8) * 2),
+            (uint32_t)ks * BK * 2);
+    }
+  }
 
   // ---- issue cursor: global step ig = (local tile it, step ikt)
   AWalk<ONE, RA, BK> aw;
@@ -898,8 +922,10 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
     unsigned char* Bs = As + BM * RB_;
     if (p.variant != 298) {   // 298: microbenchmark hook, no operand traffic (times the rest)
       aw.step(p, ikt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * RPI * RB_, vo, so); });
+      if constexpr (WS == 0) {
 #pragma unroll
-      for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * RPI * RB_, b_off[j], (uint32_t)ikt * BK * 2);
+        for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * RPI * RB_, b_off[j], (uint32_t)ikt * BK * 2);
+      }
     }
     ++ig;
     if (++ikt == nk) { ikt = 0; ++it; }
@@ -917,7 +943,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
       const int col = cn0 + wn * WTN + j * 16 + g * 4;
       f4 bv;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? bias_l[col + e] : 0.0f;
+      for (int e = 0; e < 4; ++e) bv[e] = WS ? bias_r[WS ? j : 0][e] : (col + e < p.cout ? bias_l[col + e] : 0.0f);
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) acc[j][ii] = bv;
     }
@@ -986,7 +1012,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 76 * 
     __builtin_amdgcn_s_barrier();
     if (ig < nsteps) issue_next();   // refills the slot every wave finished reading at step gs-1
     const unsigned char* As = smem + (gs % STAGES) * STAGE;
-    const unsigned char* Bs = As + BM * RB_;
+    const unsigned char* Bs = WS ? wl + ckt * BN * RB_ : As + BM * RB_;
     // every fragment of the step is read up front: the second sub-step's reads are in flight under
     // the first sub-step's MFMAs
     constexpr int NSB = BK / 32;
@@ -1798,6 +1824,22 @@ hipError_t launch_pp(const ConvParams& p, int occ, hipStream_t st) {
   return hipGetLastError();
 }
 
+// the weight-stationary 1x1 ring (one N tile, whole K in LDS)
+template <int BM, int BN, int WM, int WN, int KS>
+hipError_t launch_pring_ws(const ConvParams& p, hipStream_t st) {
+  if (p.cout > BN || p.cout % 8 || p.yoff % 8 || p.yc % 8 || p.kpad > KS * 64 || p.k != 1 || p.s != 1 || p.pad)
+    return hipErrorInvalidValue;
+  const long T = (long)((p.M + BM - 1) / BM);
+  const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
+  if (p.act == 1)
+    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, 2, true, 1, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  else if (p.act == 2)
+    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, 2, true, 2, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  else
+    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, 2, true, 0, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  return hipGetLastError();
+}
+
 // occ: resident blocks per CU the grid is sized for
 template <int BM, int BN, int WM, int WN, int STAGES, int BK = 64>
 hipError_t launch_pring(const ConvParams& p, bool one, int occ, hipStream_t st) {
@@ -1960,6 +2002,12 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // 128-input 3x3 layers stay on the 2-phase ring (1x1 256->256 @160 199 -> 216, 3x3 128->256 @80
     // 137 -> 144).  YV7_P8=0: off.
     static const int p8 = [] { const char* e = getenv("YV7_P8"); return e ? atoi(e) : 1; }();
+    // Weight-stationary 1x1 (K <= 256, 128 < cout <= 256, >= 80x80 at bs 32; tune_ops, us): 256->256
+    // @160 213 -> 201, @80 70 -> 66 / 66 -> 65; narrower or lower-resolution 1x1 layers lose.
+    // YV7_WS1=0: off.
+    static const int ws1 = [] { const char* e = getenv("YV7_WS1"); return e ? atoi(e) : 1; }();
+    if (ws1 && one && p.kpad <= 256 && p.cout > 128 && p.cout <= 256 && p.M >= 204800)
+      return launch_pring_ws<128, 256, 2, 4, 4>(p, st);
     if (p8 && t256 >= 200 && p.cout >= 256 && ((one && p.K >= 1024) || (p.k == 3 && p.cin >= 256 && p.cin % BKE == 0)))
       return launch_p8(p, one, st);
     if (one) {
@@ -2000,6 +2048,11 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 223) return one ? launch_pp<256, 128, 4, 2, true>(p, 1, st) : launch_pp<256, 128, 4, 2, false>(p, 1, st);
     // 8-phase persistent ring (conv_f16_p8_kernel)
     if ((variant == 231 || variant == 233 || (variant > 240 && variant < 256)) && (one || p.cin % BKE == 0)) return launch_p8(p, one, st);
+    // weight-stationary 1x1 rings (conv_f16_pring_kernel, WS): 234 = 128 x 256 tiles (K <= 256),
+    // 235 = 256 x 128 (K <= 256), 236 = 128 x 128 (K <= 512)
+    if (variant == 234 && one && p.cout <= 256 && p.kpad <= 256) return launch_pring_ws<128, 256, 2, 4, 4>(p, st);
+    if (variant == 235 && one && p.cout <= 128 && p.kpad <= 256) return launch_pring_ws<256, 128, 4, 2, 4>(p, st);
+    if (variant == 236 && one && p.cout <= 128 && p.kpad <= 512) return launch_pring_ws<128, 128, 2, 4, 8>(p, st);
     if (variant == 232 && (one || p.cin % BKE == 0)) return launch_p8n(p, one, st);
   }
   if (!det && p.cout > 32) {
