@@ -2059,7 +2059,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/
     // convbench.hip, bs 32, same box: @320 423 -> 337 us, @160 95 -> 79 us vs the halo kernel; @80,
     // 3 tiles per CU, its prologue does not amortise); 12-16 are its microbenchmark hooks
-    if (((variant == 0 && (long)p.B * (p.H / 16) * (p.W / 16) >= 2048) || (variant >= 11 && variant <= 16)) &&
+    if (((variant == 0 && (long)p.B * (p.H / 16) * (p.W / 16) >= 2048) || (variant >= 11 && variant <= 19)) &&
         ws64_supported(p))
       return launch_conv_ws64(p, st);
     if ((variant == 0 || variant == 10) && halo_supported(p)) return launch_conv_halo(p, st);

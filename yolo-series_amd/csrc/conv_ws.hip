@@ -51,7 +51,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint3
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, vo, so, 0, 0);
 }
 
-template <int ACT>
+// SCHED (experiments, variants 17-19): 0 = the MFMA / ds_read / VALU issue pattern below, 1 = no
+// scheduling directives, 2 = MFMA / ds_read interleave only, 3 = pattern + s_setprio around the MFMAs
+template <int ACT, int SCHED = 0>
 __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
   unsigned char* wl = smem + 2 * PBUF;
@@ -153,6 +155,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
       auto& wn = (ss & 1) ? wA : wB;
       auto& xn = (ss & 1) ? xA : xB;
       if (ss + 1 < 6) load_ss(pb, ss + 1, wn, xn);
+      if constexpr (SCHED == 3) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -161,16 +164,19 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
           for (int i = 0; i < 4; ++i)
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wc[r][j]),
                                                                __builtin_bit_cast(h8, xc[i + r]), acc[j][i], 0, 0, 0);
+      if constexpr (SCHED == 3) __builtin_amdgcn_s_setprio(0);
       side(ss);
       // issue pattern of the super-step: the next set's 18 fragment reads ride between the first 18
       // MFMAs (their latency hides under the other 30), the side work's VALU ops two per MFMA
+      if constexpr (SCHED != 1) {
 #pragma unroll
-      for (int k = 0; k < 48; ++k) {
-        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-        if (k < 18 && ss + 1 < 6) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        for (int k = 0; k < 48; ++k) {
+          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+          if (k < 18 && ss + 1 < 6) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+          if constexpr (SCHED != 2) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
       }
-      __builtin_amdgcn_sched_barrier(0);
     }
   };
   // epilogue piece q (0..7) of a finished tile: pixel row i = q / 2, channel pair (ja, jb) =
@@ -283,6 +289,12 @@ hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st) {
   if (!ws64_supported(p)) return hipErrorInvalidValue;
   const int T = p.B * (p.H / TS) * (p.W / TS);
   const int grid = T < num_cus() ? T : num_cus();
+  if (p.act == 1 && p.variant >= 17 && p.variant <= 19) {   // scheduling experiments (SiLU layers)
+    if (p.variant == 17) hipLaunchKernelGGL((conv3x3_ws64_kernel<1, 1>), dim3(grid), dim3(NT), 0, st, p);
+    else if (p.variant == 18) hipLaunchKernelGGL((conv3x3_ws64_kernel<1, 2>), dim3(grid), dim3(NT), 0, st, p);
+    else hipLaunchKernelGGL((conv3x3_ws64_kernel<1, 3>), dim3(grid), dim3(NT), 0, st, p);
+    return hipGetLastError();
+  }
   if (p.act == 1) hipLaunchKernelGGL((conv3x3_ws64_kernel<1>), dim3(grid), dim3(NT), 0, st, p);
   else if (p.act == 2) hipLaunchKernelGGL((conv3x3_ws64_kernel<2>), dim3(grid), dim3(NT), 0, st, p);
   else hipLaunchKernelGGL((conv3x3_ws64_kernel<0>), dim3(grid), dim3(NT), 0, st, p);
