@@ -1272,7 +1272,8 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   constexpr int BM = 256, BN = 256, NTH = 512;
   constexpr int HALF = 128 * 128;                    // bytes per half-tile
   constexpr int BUF = 4 * HALF;                      // one K-tile: A0 A1 B0 B1
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + 4096];
+  constexpr bool SK = (OPT & 32) != 0;               // stream-K: even K-tile ranges over the grid
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + 4096 + 16];
   float* bias_l = reinterpret_cast<float*>(smem + 2 * BUF);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1288,9 +1289,17 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   const int nk = p.kpad / BKE;
   // persistent tile order: XCD-major (OPT 4, xcd_tile_walk), else tiles blockIdx, + G, ...
   const TileWalk tw = (OPT & 4) ? xcd_tile_walk(T) : TileWalk{(int)blockIdx.x, G, T};
-  const int ntl = tw.count();
-  if (ntl == 0) return;
-  const int total = ntl * nk;                        // K-tiles this block computes
+  int ntl = tw.count();
+  int total = ntl * nk;                              // K-tiles this block computes
+  // stream-K (OPT 32): the T*nk K-tiles of the layer, tile-major, split evenly over the G blocks (XCD-
+  // major virtual order, so a tile's blocks are neighbours); tiles cut between blocks are finished by
+  // their last-arriving block from the others' fp32 partials (handoff below)
+  const long TK = (long)T * nk;
+  const int vbk = G % 8 == 0 ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int g0 = SK ? (int)(vbk * TK / G) : 0;
+  if constexpr (SK) total = (int)((vbk + 1) * TK / G) - g0;
+  if (total == 0) return;
+  auto tile_at = [&](int it) { return SK ? it : tw.at(it); };
 
   const auto xr = make_rsrc(p.x, p.xbytes);
   const auto wr = make_rsrc(p.w, p.wbytes);
@@ -1298,20 +1307,22 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
 
   // ---- staging cursors (A and B halves are staged in different phases, each in K-tile order)
-  int a_it = 0, a_kt = 0, b_it = 0, b_kt = 0, a_gk = 0, b_gk = 0;
+  int a_it = SK ? g0 / nk : 0, a_kt = SK ? g0 % nk : 0, b_it = a_it, b_kt = a_kt, a_gk = 0, b_gk = 0;
+  bool a_new = true, b_new = true;   // first staging: the block may start inside a tile (stream-K)
   uint32_t a_off[2][2], b_off[2][2], a_so = 0;
   KCursor<BKE> su;
   auto stage_a = [&](int h) {   // half h (0 / 1) of K-tile a_gk
     if (h == 0) {
-      if (a_kt == 0) {
-        const int t = tw.at(a_it);
+      if (a_kt == 0 || a_new) {
+        a_new = false;
+        const int t = tile_at(a_it);
         PixelWalk pw(p, (t / nN) * BM + wave * 8 + lr);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
           if (q) pw.advance(p, 64);
           a_off[q >> 1][q & 1] = a_origin(p, pw.b, pw.ho, pw.wo, c);
         }
-        su.init(p, 0);
+        su.init(p, a_kt * BKE);
       }
       a_so = ONE ? (uint32_t)a_kt * BKE * 2 : su.offset(p);
       if (!ONE) su.advance(p);
@@ -1326,8 +1337,9 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   };
   constexpr int BFIRST = (OPT & 16) ? 0 : 1;   // which B half of a K-tile is staged first
   auto stage_b = [&](int h) {   // half h of K-tile b_gk; staged B1 first, then B0 (OPT 16: B0, then B1)
-    if (h == BFIRST && b_kt == 0) {
-      const int n0 = tw.at(b_it) % nN * BN;
+    if (h == BFIRST && (b_kt == 0 || b_new)) {
+      b_new = false;
+      const int n0 = tile_at(b_it) % nN * BN;
 #pragma unroll
       for (int q = 0; q < 4; ++q)
         b_off[q >> 1][q & 1] = (uint32_t)(((n0 + (q >> 1) * 128 + ((q & 1) * 8 + wave) * 8 + lr) * p.kpad + c * 8) * 2);
@@ -1344,8 +1356,8 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   // ---- compute side
   f4 acc[2][2][2][4];
   int cm0 = 0, cn0 = 0;
-  auto init_tile = [&](int i) {
-    const int t = tw.at(i);
+  auto init_tile = [&](int i, bool with_bias = true) {
+    const int t = tile_at(i);
     cm0 = (t / nN) * BM;
     cn0 = (t % nN) * BN;
 #pragma unroll
@@ -1355,7 +1367,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
         const int col = cn0 + hb * 128 + wn * 32 + j * 16 + g * 4;
         f4 bv;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? bias_l[col + e] : 0.0f;
+        for (int e = 0; e < 4; ++e) bv[e] = (with_bias && col + e < p.cout) ? bias_l[col + e] : 0.0f;
 #pragma unroll
         for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
@@ -1363,6 +1375,25 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       }
   };
   const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
+  // stream-K: the last arriver's epilogue sums the tile's segments (block order) fragment by fragment
+  struct SkSum { int nseg = 0, sown = 0, blo = 0; bool blo_first = false; };
+  SkSum sks;
+  const auto prs = make_rsrc(p.part, 0x7fffffffu);
+  auto seg_sum = [&](const f4& own, int q) -> f4 {
+    f4 v = own;
+    for (int s2 = 0; s2 < sks.nseg; ++s2) {
+      f4 x;
+      if (s2 == sks.sown) {
+        x = own;
+      } else {
+        const uint32_t sl = (uint32_t)((sks.blo + s2) * 2 + ((s2 == 0 && !sks.blo_first) ? 1 : 0));
+        x = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(prs, ((sl * 32 + q) * NTH + tid) * 16, 0,
+                                                                         CPOL_SC1));
+      }
+      v = s2 == 0 ? x : v + x;
+    }
+    return v;
+  };
   auto epilogue = [&]() {
 #pragma unroll
     for (int ha = 0; ha < 2; ++ha) {
@@ -1377,10 +1408,15 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
           typedef _Float16 h4 __attribute__((ext_vector_type(4)));
           typedef uint32_t u2 __attribute__((ext_vector_type(2)));
           h4 va, vb;
+          f4 a0 = acc[hb][0][ha][i], a1 = acc[hb][1][ha][i];
+          if (SK && sks.nseg > 1) {
+            a0 = seg_sum(a0, ((hb * 2 + 0) * 2 + ha) * 4 + i);
+            a1 = seg_sum(a1, ((hb * 2 + 1) * 2 + ha) * 4 + i);
+          }
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            va[e] = (_Float16)act_t<ACT>(acc[hb][0][ha][i][e]);
-            vb[e] = (_Float16)act_t<ACT>(acc[hb][1][ha][i][e]);
+            va[e] = (_Float16)act_t<ACT>(a0[e]);
+            vb[e] = (_Float16)act_t<ACT>(a1[e]);
           }
           const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
           const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
@@ -1392,6 +1428,45 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
         }
       }
     }
+  };
+
+  // stream-K hand-off of a tile cut between blocks (the split-K protocol of splitk_reduce: sc1 partial
+  // stores, every wave's vmcnt(0), a barrier, one lane's agent-scope atomic; the last arriver sums the
+  // segments in block order — the result does not depend on arrival order — and runs the epilogue).
+  // The two stagger groups are aligned around it (group 0 waits one barrier first, group 1 one after).
+  auto handoff = [&](int t, bool first) {
+    if (wm == 0) __builtin_amdgcn_s_barrier();
+    const uint32_t slot = (uint32_t)(vbk * 2 + (first ? 0 : 1));
+#pragma unroll
+    for (int q = 0; q < 32; ++q)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[q >> 4][(q >> 3) & 1][(q >> 2) & 1][q & 3]), prs,
+                                             ((slot * 32 + q) * NTH + tid) * 16, 0, CPOL_SC1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const long tk0 = (long)t * nk;
+    const int blo = (int)(((tk0 + 1) * G - 1) / TK), bhi = (int)(((tk0 + nk) * G - 1) / TK);
+    const int nseg = bhi - blo + 1;
+    int* flag = reinterpret_cast<int*>(smem + 2 * BUF + 4096);
+    if (tid == 0) {
+      const int old = __hip_atomic_fetch_add(p.cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int last = old == nseg - 1;
+      if (last) __hip_atomic_store(p.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      *flag = last;
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const bool last = *flag != 0;
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (last) {
+      sks.nseg = nseg;
+      sks.sown = vbk - blo;
+      sks.blo = blo;
+      sks.blo_first = (long)blo * TK / G == tk0;   // the tile is the first segment of block blo
+      epilogue();
+      sks.nseg = 0;
+    }
+    if (wm == 1) __builtin_amdgcn_s_barrier();
   };
 
   // ---- prologue: K-tile 0 whole, K-tile 1's A0, B1 and A1 in flight (OPT 16: all of K-tile 1)
@@ -1414,7 +1489,8 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bias_l
   __builtin_amdgcn_s_barrier();
-  init_tile(0);
+  int ci = SK ? g0 / nk : 0, ckt = SK ? g0 % nk : 0, seg0 = ckt;   // compute cursor: tile, K step, segment start
+  init_tile(ci, ckt == 0);
   if (wm == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind group 0
 
   u4 xa[2][4], wb[2][2], wb1[2][2];   // wb1: OPT 16 keeps B half 1's fragments apart from half 0's
@@ -1471,7 +1547,6 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     __builtin_amdgcn_s_barrier();
   };
 
-  int ci = 0, ckt = 0;
   if constexpr ((OPT & 16) != 0) {
     // OPT 16: B half 0's fragments stay in registers from phase 0 to phase 3, so A0 and B0 are both
     // free after phase 0: K-tile k+2 is staged whole in phases 1-3 (A0+B0, B1, A1) and the tile
@@ -1541,14 +1616,27 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     mfma_q(1, 0);
-    if (++ckt == nk) {
-      epilogue();
-      ckt = 0;
-      if (++ci < ntl) init_tile(ci);
+    const bool tend = ++ckt == nk, rend = k == total - 1;
+    if (tend || (SK && rend)) {
+      if (!SK || (seg0 == 0 && tend)) epilogue();
+      else handoff(tile_at(ci), (long)tile_at(ci) * nk + seg0 == g0);
+      if (tend && !rend) {
+        ckt = 0;
+        seg0 = 0;
+        init_tile(++ci);
+      }
     }
   }
   if (wm == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts in both groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+template <bool ONE>
+hipError_t launch_p8_sk(const ConvParams& p, int grid, hipStream_t st) {
+  if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, 36>), dim3(grid), dim3(512), 0, st, p);
+  else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 2, 36>), dim3(grid), dim3(512), 0, st, p);
+  else hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 0, 36>), dim3(grid), dim3(512), 0, st, p);
+  return hipGetLastError();
 }
 
 template <bool ONE>
@@ -1795,10 +1883,43 @@ int device_cus() {
 }
 
 // the 8-phase persistent ring: uniform K steps only (1x1, or cin % 64 == 0)
+int env_variant() {
+  static const int v = [] { const char* e = getenv("YV7_CONV_F16"); return e ? atoi(e) : 0; }();
+  return v;
+}
+
+constexpr size_t P8_PART = 256 * 256 * 4;   // one fp32 partial 256 x 256 tile (stream-K hand-off)
+
+// The dispatch's 8-phase-ring rule (launch_conv_f16 quotes the measurements behind it).
+bool p8_default(const ConvParams& p) {
+  static const int on = [] { const char* e = getenv("YV7_P8"); return e ? atoi(e) : 1; }();
+  const bool one = p.k == 1 && p.s == 1 && p.pad == 0;
+  const long t256 = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
+  return on && !p.pool && p.cout >= 256 && p.cout <= 1024 && p.cout % 8 == 0 && t256 >= 200 &&
+         ((one && p.K >= 1024) || (p.k == 3 && p.cin >= 256 && p.cin % BKE == 0));
+}
+
+// Stream-K form of the 8-phase ring (variant 237, or the dispatch with YV7_P8SK=1): the grid is every CU
+// and the layer's K-tiles are split evenly over it, so a layer with 200 tiles of 256 x 256 no longer
+// leaves 56 CUs idle; needs the split-K scratch (one partial tile per block and segment end).
+bool p8_streamk(const ConvParams& p) {
+  static const int sk = [] { const char* e = getenv("YV7_P8SK"); return e ? atoi(e) : 0; }();
+  const int variant = p.variant ? p.variant : env_variant();
+  return variant == 237 || (variant == 0 && sk && p8_default(p));
+}
+
 hipError_t launch_p8(const ConvParams& p, bool one, hipStream_t st) {
   if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || (!one && p.cin % BKE)) return hipErrorInvalidValue;
   const long T = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
-  const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
+  const int cus = device_cus();
+  if (p8_streamk(p) && p.part && p.cnt && p.part_bytes >= (size_t)cus * 2 * P8_PART && p.cnt_n >= T) {
+    // at most one block per K-tile: every block's range is non-empty, so the blocks between a tile's
+    // first and last are exactly its segments
+    const long TK = T * (p.kpad / BKE);
+    const int grid = (int)(TK < (long)cus ? TK : (long)cus);
+    return one ? launch_p8_sk<true>(p, grid, st) : launch_p8_sk<false>(p, grid, st);
+  }
+  const int grid = (int)(T < (long)cus ? T : (long)cus);
   return one ? launch_p8_t<true>(p, grid, st) : launch_p8_t<false>(p, grid, st);
 }
 
@@ -1883,10 +2004,6 @@ struct Choice {
   int S = 1;      // K splits
 };
 
-int env_variant() {
-  static const int v = [] { const char* e = getenv("YV7_CONV_F16"); return e ? atoi(e) : 0; }();
-  return v;
-}
 
 long ring_tiles(const ConvParams& p, int cfg) {
   return (long)((p.M + cfg_bm[cfg] - 1) / cfg_bm[cfg]) * ((p.cout + cfg_bn[cfg] - 1) / cfg_bn[cfg]);
@@ -1959,12 +2076,14 @@ hipError_t launch_choice(const ConvParams& p, const Choice& c, bool one, hipStre
 }  // namespace
 
 size_t conv_splitk_part_bytes(const ConvParams& p) {
+  if (!p.pool && p8_streamk(p)) return (size_t)device_cus() * 2 * P8_PART;
   const Choice c = choose(p, false);   // (choose() keeps this under 2 GiB)
   if (c.cfg < 0 || c.S <= 1) return 0;
   return (size_t)ring_tiles(p, c.cfg) * c.S * cfg_bm[c.cfg] * cfg_bn[c.cfg] * 4;
 }
 
 int conv_splitk_tiles(const ConvParams& p) {
+  if (!p.pool && p8_streamk(p)) return (int)(((p.M + 255) / 256) * ((p.cout + 255) / 256));
   const Choice c = choose(p, false);
   return (c.cfg < 0 || c.S <= 1) ? 0 : (int)ring_tiles(p, c.cfg);
 }
@@ -2001,15 +2120,14 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // 1024->1024 @40 142 -> 138, 1024->512 @40 74 -> 70, 1024->256 @40 41 -> 39.  Short-K 1x1 and
     // 128-input 3x3 layers stay on the 2-phase ring (1x1 256->256 @160 199 -> 216, 3x3 128->256 @80
     // 137 -> 144).  YV7_P8=0: off.
-    static const int p8 = [] { const char* e = getenv("YV7_P8"); return e ? atoi(e) : 1; }();
+
     // Weight-stationary 1x1 (K <= 256, 128 < cout <= 256, >= 80x80 at bs 32; tune_ops, us): 256->256
     // @160 213 -> 201, @80 70 -> 66 / 66 -> 65; narrower or lower-resolution 1x1 layers lose.
     // YV7_WS1=0: off.
     static const int ws1 = [] { const char* e = getenv("YV7_WS1"); return e ? atoi(e) : 1; }();
     if (ws1 && one && p.kpad <= 256 && p.cout > 128 && p.cout <= 256 && p.M >= 204800)
       return launch_pring_ws<128, 256, 2, 4, 4>(p, st);
-    if (p8 && t256 >= 200 && p.cout >= 256 && ((one && p.K >= 1024) || (p.k == 3 && p.cin >= 256 && p.cin % BKE == 0)))
-      return launch_p8(p, one, st);
+    if (p8_default(p)) return launch_p8(p, one, st);
     if (one) {
       if (p.K >= 256 && p.cout >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
       if (wide && p.cout >= 256 && t256 >= 200) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
@@ -2047,7 +2165,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 222) return one ? launch_pp<128, 128, 2, 2, true>(p, 2, st) : launch_pp<128, 128, 2, 2, false>(p, 2, st);
     if (variant == 223) return one ? launch_pp<256, 128, 4, 2, true>(p, 1, st) : launch_pp<256, 128, 4, 2, false>(p, 1, st);
     // 8-phase persistent ring (conv_f16_p8_kernel)
-    if ((variant == 231 || variant == 233 || (variant > 240 && variant < 256)) && (one || p.cin % BKE == 0)) return launch_p8(p, one, st);
+    if ((variant == 231 || variant == 233 || variant == 237 || (variant > 240 && variant < 256)) && (one || p.cin % BKE == 0))
+      return launch_p8(p, one, st);
     // weight-stationary 1x1 rings (conv_f16_pring_kernel, WS): 234 = 128 x 256 tiles (K <= 256),
     // 235 = 256 x 128 (K <= 256), 236 = 128 x 128 (K <= 512)
     if (variant == 234 && one && p.cout <= 256 && p.kpad <= 256) return launch_pring_ws<128, 256, 2, 4, 4>(p, st);
