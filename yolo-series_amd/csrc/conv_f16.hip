@@ -1267,18 +1267,27 @@ __global__ __launch_bounds__(64 * WM * WN, (2 * (BM + BN) * 128 <= 76 * 1024) ? 
 // acc[hb][j][ha][i] = channels hb*128 + wn*32 + j*16 + g*4 + e of pixel ha*128 + wm*64 + i*16 + li.
 // OPT (experiments, variants 240 + OPT): 1 = DMA issued before the phase's LDS reads, 2 = no s_setprio,
 // 4 = XCD-major persistent tile order, 8 = only group 1 retires its reads before the first barrier
-template <bool ONE, int ACT, int OPT = 0>
+// BM x BN = 256 x 256 (wide layers) or 512 x 128 (128-channel layers: the same 128 x 64 output per
+// wave and 16 MFMAs per phase; A halves of 256 rows, B halves of 64, bias read from global).
+template <bool ONE, int ACT, int OPT = 0, int BM = 256, int BN = 256>
 __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p) {
-  constexpr int BM = 256, BN = 256, NTH = 512;
-  constexpr int HALF = 128 * 128;                    // bytes per half-tile
-  constexpr int BUF = 4 * HALF;                      // one K-tile: A0 A1 B0 B1
+  constexpr int NTH = 512;
+  constexpr int AHR = BM / 2, BHR = BN / 2;          // rows per A / B half-tile
+  constexpr int AHB = AHR * ROWB, BHB = BHR * ROWB;  // bytes per A / B half-tile
+  constexpr int BUF = 2 * AHB + 2 * BHB;             // one K-tile: A0 A1 B0 B1
+  constexpr int AP = AHR / 64, BP = BHR / 64;        // 1 KiB DMA pieces per wave per A / B half
+  constexpr int VMC = 2 * AP + BP;                   // loads of three half-tiles (A0, B1, A1) per wave
+  constexpr int WNC = BHR / 32;                      // waves across a B half (32 channels each)
+  static_assert(AP >= 1 && BP >= 1 && (AHR / 64) * WNC == 8, "8 waves of 64 x 32 per block quadrant");
+  constexpr int BIASB = (2 * BUF + 4096 + 16 <= 163840) ? 4096 : 0;   // bias in LDS when it fits
   constexpr bool SK = (OPT & 32) != 0;               // stream-K: even K-tile ranges over the grid
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + 4096 + 16];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + BIASB + (SK ? 16 : 0)];
   float* bias_l = reinterpret_cast<float*>(smem + 2 * BUF);
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;           // wm: the stagger group
+  const int wm = wave / WNC, wn = wave % WNC;
+  const int grp = wave >> 2;                         // stagger group (one wave of each per SIMD)
   const int g = lane >> 4, li = lane & 15;
   const int lr = lane >> 3;                          // DMA: row within an 8-row piece
   const int c = (lane & 7) ^ lr;                     // DMA: source chunk of slot lane & 7
@@ -1304,12 +1313,13 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   const auto xr = make_rsrc(p.x, p.xbytes);
   const auto wr = make_rsrc(p.w, p.wbytes);
   const auto yr = make_rsrc(p.y, 0x7fffffffu);
-  for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
+  if constexpr (BIASB != 0)
+    for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
 
   // ---- staging cursors (A and B halves are staged in different phases, each in K-tile order)
   int a_it = SK ? g0 / nk : 0, a_kt = SK ? g0 % nk : 0, b_it = a_it, b_kt = a_kt, a_gk = 0, b_gk = 0;
   bool a_new = true, b_new = true;   // first staging: the block may start inside a tile (stream-K)
-  uint32_t a_off[2][2], b_off[2][2], a_so = 0;
+  uint32_t a_off[2][AP], b_off[2][BP], a_so = 0;
   KCursor<BKE> su;
   auto stage_a = [&](int h) {   // half h (0 / 1) of K-tile a_gk
     if (h == 0) {
@@ -1318,18 +1328,18 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
         const int t = tile_at(a_it);
         PixelWalk pw(p, (t / nN) * BM + wave * 8 + lr);
 #pragma unroll
-        for (int q = 0; q < 4; ++q) {
+        for (int q = 0; q < 2 * AP; ++q) {
           if (q) pw.advance(p, 64);
-          a_off[q >> 1][q & 1] = a_origin(p, pw.b, pw.ho, pw.wo, c);
+          a_off[q / AP][q % AP] = a_origin(p, pw.b, pw.ho, pw.wo, c);
         }
         su.init(p, a_kt * BKE);
       }
       a_so = ONE ? (uint32_t)a_kt * BKE * 2 : su.offset(p);
       if (!ONE) su.advance(p);
     }
-    unsigned char* d = smem + (a_gk & 1) * BUF + h * HALF;
+    unsigned char* d = smem + (a_gk & 1) * BUF + h * AHB;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) dma16(xr, d + (j * 8 + wave) * 8 * ROWB, a_off[h][j], a_so);
+    for (int j = 0; j < AP; ++j) dma16(xr, d + (j * 8 + wave) * 8 * ROWB, a_off[h][j], a_so);
     if (h == 1) {
       ++a_gk;
       if (++a_kt == nk) { a_kt = 0; ++a_it; }
@@ -1341,12 +1351,13 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       b_new = false;
       const int n0 = tile_at(b_it) % nN * BN;
 #pragma unroll
-      for (int q = 0; q < 4; ++q)
-        b_off[q >> 1][q & 1] = (uint32_t)(((n0 + (q >> 1) * 128 + ((q & 1) * 8 + wave) * 8 + lr) * p.kpad + c * 8) * 2);
+      for (int q = 0; q < 2 * BP; ++q)
+        b_off[q / BP][q % BP] =
+            (uint32_t)(((n0 + (q / BP) * BHR + ((q % BP) * 8 + wave) * 8 + lr) * p.kpad + c * 8) * 2);
     }
-    unsigned char* d = smem + (b_gk & 1) * BUF + (2 + h) * HALF;
+    unsigned char* d = smem + (b_gk & 1) * BUF + 2 * AHB + h * BHB;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) dma16(wr, d + (j * 8 + wave) * 8 * ROWB, b_off[h][j], (uint32_t)b_kt * BKE * 2);
+    for (int j = 0; j < BP; ++j) dma16(wr, d + (j * 8 + wave) * 8 * ROWB, b_off[h][j], (uint32_t)b_kt * BKE * 2);
     if (h != BFIRST) {
       ++b_gk;
       if (++b_kt == nk) { b_kt = 0; ++b_it; }
@@ -1364,10 +1375,11 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     for (int hb = 0; hb < 2; ++hb)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        const int col = cn0 + hb * 128 + wn * 32 + j * 16 + g * 4;
+        const int col = cn0 + hb * BHR + wn * 32 + j * 16 + g * 4;
         f4 bv;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) bv[e] = (with_bias && col + e < p.cout) ? bias_l[col + e] : 0.0f;
+        for (int e = 0; e < 4; ++e)
+          bv[e] = (with_bias && col + e < p.cout) ? (BIASB ? bias_l[col + e] : p.bias[col + e]) : 0.0f;
 #pragma unroll
         for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
@@ -1397,11 +1409,11 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   auto epilogue = [&]() {
 #pragma unroll
     for (int ha = 0; ha < 2; ++ha) {
-      PixelWalk pw(p, cm0 + ha * 128 + wm * 64 + li);
+      PixelWalk pw(p, cm0 + ha * AHR + wm * 64 + li);
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if (i) pw.advance(p, 16);
-        const int m = cm0 + ha * 128 + wm * 64 + i * 16 + li;
+        const int m = cm0 + ha * AHR + wm * 64 + i * 16 + li;
         const uint32_t yo = (uint32_t)((pix_index(pw.b, pw.ho, pw.wo, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
 #pragma unroll
         for (int hb = 0; hb < 2; ++hb) {
@@ -1422,7 +1434,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
           const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
           const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
           const u4 v = {s0[0], s1[0], s0[1], s1[1]};
-          const int n = cn0 + hb * 128 + wn * 32 + (int)lane_ch;
+          const int n = cn0 + hb * BHR + wn * 32 + (int)lane_ch;
           const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
           __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
         }
@@ -1435,7 +1447,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   // segments in block order — the result does not depend on arrival order — and runs the epilogue).
   // The two stagger groups are aligned around it (group 0 waits one barrier first, group 1 one after).
   auto handoff = [&](int t, bool first) {
-    if (wm == 0) __builtin_amdgcn_s_barrier();
+    if (grp == 0) __builtin_amdgcn_s_barrier();
     const uint32_t slot = (uint32_t)(vbk * 2 + (first ? 0 : 1));
 #pragma unroll
     for (int q = 0; q < 32; ++q)
@@ -1446,7 +1458,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     const long tk0 = (long)t * nk;
     const int blo = (int)(((tk0 + 1) * G - 1) / TK), bhi = (int)(((tk0 + nk) * G - 1) / TK);
     const int nseg = bhi - blo + 1;
-    int* flag = reinterpret_cast<int*>(smem + 2 * BUF + 4096);
+    int* flag = reinterpret_cast<int*>(smem + 2 * BUF + BIASB);
     if (tid == 0) {
       const int old = __hip_atomic_fetch_add(p.cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const int last = old == nseg - 1;
@@ -1466,11 +1478,12 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       epilogue();
       sks.nseg = 0;
     }
-    if (wm == 1) __builtin_amdgcn_s_barrier();
+    if (grp == 1) __builtin_amdgcn_s_barrier();
   };
 
   // ---- prologue: K-tile 0 whole, K-tile 1's A0, B1 and A1 in flight (OPT 16: all of K-tile 1)
   if constexpr ((OPT & 16) != 0) {
+    static_assert((OPT & 16) == 0 || (BM == 256 && BN == 256), "OPT 16: 256 x 256 tiles only");
     stage_a(0); stage_b(0); stage_b(1); stage_a(1);
     if (total > 1) {
       stage_a(0); stage_b(0); stage_b(1); stage_a(1);
@@ -1482,7 +1495,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   stage_a(0); stage_b(1); stage_a(1); stage_b(0);
   if (total > 1) {
     stage_a(0); stage_b(1); stage_a(1);
-    asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
@@ -1491,7 +1504,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   __builtin_amdgcn_s_barrier();
   int ci = SK ? g0 / nk : 0, ckt = SK ? g0 % nk : 0, seg0 = ckt;   // compute cursor: tile, K step, segment start
   init_tile(ci, ckt == 0);
-  if (wm == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind group 0
+  if (grp == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind group 0
 
   u4 xa[2][4], wb[2][2], wb1[2][2];   // wb1: OPT 16 keeps B half 1's fragments apart from half 0's
   auto read_a = [&](const unsigned char* h) {
@@ -1530,7 +1543,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     __builtin_amdgcn_s_barrier();
   };
   auto mfma_q = [&](int ha, int hb) {
-    if (!(OPT & 8) || wm == 1)
+    if (!(OPT & 8) || grp == 1)
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this phase's reads retired (WAR: see above)
     __builtin_amdgcn_s_barrier();
     if (!(OPT & 2)) __builtin_amdgcn_s_setprio(1);
@@ -1556,13 +1569,13 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     for (int k = 0; k < total; ++k) {
       const unsigned char* bk = smem + (k & 1) * BUF;
       const bool n2 = k + 2 < total;
-      read_b_to(bk + 2 * HALF, wb);
+      read_b_to(bk + 2 * AHB, wb);
       read_a(bk);
       mfma_qw(0, 0, wb);
-      read_b_to(bk + 3 * HALF, wb1);
+      read_b_to(bk + 2 * AHB + BHB, wb1);
       if (n2) { stage_a(0); stage_b(0); }
       mfma_qw(0, 1, wb1);
-      read_a(bk + HALF);
+      read_a(bk + AHB);
       if (n2) stage_b(1);
       mfma_qw(1, 1, wb1);
       if (n2) stage_a(1);
@@ -1582,7 +1595,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
         if (++ci < ntl) init_tile(ci);
       }
     }
-    if (wm == 0) __builtin_amdgcn_s_barrier();
+    if (grp == 0) __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     return;
   }
@@ -1592,26 +1605,26 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     constexpr bool DF = (OPT & 1) != 0;   // DMA first
     // phase 0: quadrant (0,0)
     if (DF && n1) stage_b(0);
-    read_b(bk + 2 * HALF);
+    read_b(bk + 2 * AHB);
     read_a(bk);
     if (!DF && n1) stage_b(0);
     mfma_q(0, 0);
     // phase 1: (0,1)
     if (DF && n2) stage_a(0);
-    read_b(bk + 3 * HALF);
+    read_b(bk + 2 * AHB + BHB);
     if (!DF && n2) stage_a(0);
     mfma_q(0, 1);
     // phase 2: (1,1)
     if (DF && n2) stage_b(1);
-    read_a(bk + HALF);
+    read_a(bk + AHB);
     if (!DF && n2) stage_b(1);
     mfma_q(1, 1);
     // phase 3: (1,0); K-tile k+1 retired (k+2's A0, B1 and A1 may stay in flight)
     if (DF && n2) stage_a(1);
-    read_b(bk + 2 * HALF);
+    read_b(bk + 2 * AHB);
     if (n2) {
       if (!DF) stage_a(1);
-      asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
@@ -1627,7 +1640,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       }
     }
   }
-  if (wm == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts in both groups
+  if (grp == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts in both groups
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -1923,6 +1936,23 @@ hipError_t launch_p8(const ConvParams& p, bool one, hipStream_t st) {
   return one ? launch_p8_t<true>(p, grid, st) : launch_p8_t<false>(p, grid, st);
 }
 
+// the 8-phase ring on 512 x 128 tiles (128-channel layers)
+hipError_t launch_p8w(const ConvParams& p, bool one, hipStream_t st) {
+  if (p.cout > 128 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || (!one && p.cin % BKE)) return hipErrorInvalidValue;
+  const long T = (long)((p.M + 511) / 512);
+  const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
+  if (one) {
+    if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<true, 1, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<true, 2, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((conv_f16_p8_kernel<true, 0, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+  } else {
+    if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<false, 1, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<false, 2, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    else hipLaunchKernelGGL((conv_f16_p8_kernel<false, 0, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+  }
+  return hipGetLastError();
+}
+
 hipError_t launch_p8n(const ConvParams& p, bool one, hipStream_t st) {
   if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || (!one && p.cin % BKE)) return hipErrorInvalidValue;
   const long T = (long)((p.M + 255) / 256) * ((p.cout + 127) / 128);
@@ -2173,6 +2203,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 235 && one && p.cout <= 128 && p.kpad <= 256) return launch_pring_ws<256, 128, 4, 2, 4>(p, st);
     if (variant == 236 && one && p.cout <= 128 && p.kpad <= 512) return launch_pring_ws<128, 128, 2, 4, 8>(p, st);
     if (variant == 232 && (one || p.cin % BKE == 0)) return launch_p8n(p, one, st);
+    if (variant == 238 && p.cout <= 128 && (one || p.cin % BKE == 0)) return launch_p8w(p, one, st);
   }
   if (!det && p.cout > 32) {
     // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/
