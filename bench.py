@@ -366,10 +366,12 @@ def main(argv=None):
             step()
         graph.replay()
         torch.cuda.synchronize()
-    # Live per-op HIP events inside the timed region: libyv7's profile mode records an event before the
-    # first op and after every op of the first n_live timed forwards, on the stream each forward runs on
-    # (with batches in flight the three streams' kernels share the chip, so these are the durations of the
-    # timed regime, contention included).  Not under --graph / --split.
+    # Live per-op HIP events inside the timed region: libyv7's profile mode launches every op of the
+    # first n_live timed forwards with a (start, stop) event pair on the op's own kernel dispatches
+    # (hipExtLaunchKernel), so a duration is the kernel's begin .. end as rocprofv3 reports it — with
+    # batches in flight the three streams' kernels share the chip, so these are the durations of the
+    # timed regime, contention included, but not the time a kernel waits in its queue for CUs the
+    # other streams hold.  Not under --graph / --split.
     n_live = 0 if (a.no_live_events or nsplit > 1 or graph is not None) else min(a.steps, a.live_forwards)
     plan.profile_enable(n_live)
     if distributed:
@@ -471,9 +473,10 @@ def main(argv=None):
                          'kernel': 'conv kernels (MFMA implicit-GEMM ring / persistent ring / weight-stationary '
                                    '3x3 / halo; all CONV and DETECT launches of the forward)',
                          'launches_per_forward': nconv, 'mean_launch_us': round(mean_launch_s * 1e6, 2),
-                         'timing': (f'HIP events around every op of {nf} forwards inside the timed region, on '
-                                    f'each forward\'s stream ({nstreams} stream(s) in flight)') if nf else
-                                   'HIP events around every op of 2 serial forwards after the timed region',
+                         'timing': (f'HIP event pair on every op\'s own kernel dispatches (hipExtLaunchKernel: '
+                                    f'dispatch begin .. end, as rocprofv3 reports) for {nf} forwards inside the '
+                                    f'timed region ({nstreams} stream(s) in flight)') if nf else
+                                   'HIP event pairs on every op of 2 serial forwards after the timed region',
                          'algorithmic_bytes_per_launch': round(bytes_per_launch),
                          'mfma_tflops': round(achieved_tf, 1),
                          'mfma_frac': round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4),

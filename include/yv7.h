@@ -150,9 +150,11 @@ int yv7_forward(yv7_plan* plan, const void* x, int x_dtype, int B, int H, int W,
 int yv7_set_op_variant(yv7_plan* plan, int op, int variant);
 
 /* Live per-op timing: with max_forwards > 0 every following yv7_forward (up to max_forwards of
- * them) records one HIP event before its first op and one after each op on its stream; 0 turns it
- * off and frees the events.  yv7_profile_read synchronizes on the recorded events and returns, per
- * op, the elapsed milliseconds summed over the recorded forwards (op_ms: [n_ops]). */
+ * them) launches each op's kernels with a (start, stop) HIP event pair (hipExtLaunchKernel: the
+ * first kernel's dispatch begin, the last kernel's end — the interval rocprofv3's kernel trace
+ * reports); an op that launches nothing records both events back to back.  0 turns it off and frees
+ * the events.  yv7_profile_read synchronizes on the recorded events and returns, per op, the elapsed
+ * milliseconds summed over the recorded forwards (op_ms: [n_ops]). */
 int yv7_profile_enable(yv7_plan* plan, int max_forwards);
 int yv7_profile_read(yv7_plan* plan, int* n_forwards, float* op_ms);
 

@@ -242,7 +242,7 @@ __global__ __launch_bounds__(NT) void conv_kernel(const ConvParams p) {
 template <typename T, int BM, int BN, bool ONE, bool DET>
 hipError_t launch_t(const ConvParams& p, hipStream_t st) {
   const int nM = (p.M + BM - 1) / BM, nN = (p.cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_kernel<T, BM, BN, ONE, DET>), dim3(nM * nN), dim3(NT), 0, st, p);
+  YV7_LAUNCH((conv_kernel<T, BM, BN, ONE, DET>), dim3(nM * nN), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 

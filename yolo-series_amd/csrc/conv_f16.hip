@@ -1646,22 +1646,22 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
 
 template <bool ONE>
 hipError_t launch_p8_sk(const ConvParams& p, int grid, hipStream_t st) {
-  if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, 36>), dim3(grid), dim3(512), 0, st, p);
-  else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 2, 36>), dim3(grid), dim3(512), 0, st, p);
-  else hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 0, 36>), dim3(grid), dim3(512), 0, st, p);
+  if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 36>), dim3(grid), dim3(512), 0, st, p);
+  else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 2, 36>), dim3(grid), dim3(512), 0, st, p);
+  else YV7_LAUNCH((conv_f16_p8_kernel<ONE, 0, 36>), dim3(grid), dim3(512), 0, st, p);
   return hipGetLastError();
 }
 
 template <bool ONE>
 hipError_t launch_p8_t(const ConvParams& p, int grid, hipStream_t st) {
   if (p.act == 1 && p.variant == 233) {   // experiment: OPT 16 schedule (+ XCD order)
-    hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, 20>), dim3(grid), dim3(512), 0, st, p);
+    YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 20>), dim3(grid), dim3(512), 0, st, p);
     return hipGetLastError();
   }
   if (p.act == 1 && p.variant >= 241 && p.variant <= 255) {   // experiments (SiLU layers only; 244 = 231)
     switch (p.variant - 240) {
-      case 15: hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, 0>), dim3(grid), dim3(512), 0, st, p); return hipGetLastError();
-#define P8X(o) case o: hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, o>), dim3(grid), dim3(512), 0, st, p); return hipGetLastError();
+      case 15: YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 0>), dim3(grid), dim3(512), 0, st, p); return hipGetLastError();
+#define P8X(o) case o: YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, o>), dim3(grid), dim3(512), 0, st, p); return hipGetLastError();
       P8X(1) P8X(2) P8X(8) P8X(5) P8X(12) P8X(13)
       case 4: break;   // the default
 #undef P8X
@@ -1669,9 +1669,9 @@ hipError_t launch_p8_t(const ConvParams& p, int grid, hipStream_t st) {
     }
   }
   // XCD-major tile order (OPT 4): 1x1 1024->1024 @40 140 -> 133 us, 3x3 layers unchanged (tune_ops)
-  if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 1, 4>), dim3(grid), dim3(512), 0, st, p);
-  else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 2, 4>), dim3(grid), dim3(512), 0, st, p);
-  else hipLaunchKernelGGL((conv_f16_p8_kernel<ONE, 0, 4>), dim3(grid), dim3(512), 0, st, p);
+  if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 4>), dim3(grid), dim3(512), 0, st, p);
+  else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 2, 4>), dim3(grid), dim3(512), 0, st, p);
+  else YV7_LAUNCH((conv_f16_p8_kernel<ONE, 0, 4>), dim3(grid), dim3(512), 0, st, p);
   return hipGetLastError();
 }
 
@@ -1867,20 +1867,20 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
 
 template <bool ONE>
 hipError_t launch_p8n_t(const ConvParams& p, int grid, hipStream_t st) {
-  if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8n_kernel<ONE, 1>), dim3(grid), dim3(512), 0, st, p);
-  else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8n_kernel<ONE, 2>), dim3(grid), dim3(512), 0, st, p);
-  else hipLaunchKernelGGL((conv_f16_p8n_kernel<ONE, 0>), dim3(grid), dim3(512), 0, st, p);
+  if (p.act == 1) YV7_LAUNCH((conv_f16_p8n_kernel<ONE, 1>), dim3(grid), dim3(512), 0, st, p);
+  else if (p.act == 2) YV7_LAUNCH((conv_f16_p8n_kernel<ONE, 2>), dim3(grid), dim3(512), 0, st, p);
+  else YV7_LAUNCH((conv_f16_p8n_kernel<ONE, 0>), dim3(grid), dim3(512), 0, st, p);
   return hipGetLastError();
 }
 
 template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int BK>
 hipError_t launch_pring_act(const ConvParams& p, int grid, hipStream_t st) {
   if (p.act == 1)
-    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 1, BK>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 1, BK>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   else if (p.act == 2)
-    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 2, BK>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 2, BK>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   else
-    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 0, BK>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_pring_kernel<BM, BN, WM, WN, STAGES, ONE, 0, BK>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
 }
 
@@ -1942,13 +1942,13 @@ hipError_t launch_p8w(const ConvParams& p, bool one, hipStream_t st) {
   const long T = (long)((p.M + 511) / 512);
   const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
   if (one) {
-    if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<true, 1, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-    else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<true, 2, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((conv_f16_p8_kernel<true, 0, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<true, 1, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<true, 2, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    else YV7_LAUNCH((conv_f16_p8_kernel<true, 0, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
   } else {
-    if (p.act == 1) hipLaunchKernelGGL((conv_f16_p8_kernel<false, 1, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-    else if (p.act == 2) hipLaunchKernelGGL((conv_f16_p8_kernel<false, 2, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-    else hipLaunchKernelGGL((conv_f16_p8_kernel<false, 0, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<false, 1, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<false, 2, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
+    else YV7_LAUNCH((conv_f16_p8_kernel<false, 0, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
   }
   return hipGetLastError();
 }
@@ -1967,11 +1967,11 @@ hipError_t launch_pp(const ConvParams& p, int occ, hipStream_t st) {
   const long cap = (long)device_cus() * occ;
   const int grid = (int)(T < cap ? T : cap);
   if (p.act == 1)
-    hipLaunchKernelGGL((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 1>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 1>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   else if (p.act == 2)
-    hipLaunchKernelGGL((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 2>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 2>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   else
-    hipLaunchKernelGGL((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 0>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 0>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
 }
 
@@ -1983,11 +1983,11 @@ hipError_t launch_pring_ws(const ConvParams& p, hipStream_t st) {
   const long T = (long)((p.M + BM - 1) / BM);
   const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
   if (p.act == 1)
-    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, 2, true, 1, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_pring_kernel<BM, BN, WM, WN, 2, true, 1, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   else if (p.act == 2)
-    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, 2, true, 2, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_pring_kernel<BM, BN, WM, WN, 2, true, 2, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   else
-    hipLaunchKernelGGL((conv_f16_pring_kernel<BM, BN, WM, WN, 2, true, 0, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_pring_kernel<BM, BN, WM, WN, 2, true, 0, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
 }
 
@@ -2004,7 +2004,7 @@ hipError_t launch_pring(const ConvParams& p, bool one, int occ, hipStream_t st) 
 template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, bool DET = false>
 hipError_t launch_ring(const ConvParams& p, hipStream_t st) {
   const int nM = (p.M + BM - 1) / BM, nN = (p.cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, ONE, DET>), dim3(nM * nN), dim3(64 * WM * WN), 0, st, p);
+  YV7_LAUNCH((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, ONE, DET>), dim3(nM * nN), dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
 }
 
@@ -2016,7 +2016,7 @@ hipError_t launch_ring2(const ConvParams& p, bool one, hipStream_t st) {
 template <int BM, int BN, int WM, bool ONE, bool DET, int PF = 1, bool POOL = false>
 hipError_t launch_t(const ConvParams& p, hipStream_t st) {
   const int nM = (p.M + BM - 1) / BM, nN = (p.cout + BN - 1) / BN;
-  hipLaunchKernelGGL((conv_f16_kernel<BM, BN, WM, ONE, DET, PF, POOL>), dim3(nM * nN), dim3(NT), 0, st, p);
+  YV7_LAUNCH((conv_f16_kernel<BM, BN, WM, ONE, DET, PF, POOL>), dim3(nM * nN), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 
@@ -2085,9 +2085,9 @@ hipError_t launch_ring_s(const ConvParams& p0, bool one, int S, hipStream_t st) 
     return hipErrorInvalidValue;   // the caller sized the scratch with conv_splitk_part_bytes
   const unsigned nblk = (unsigned)(tiles * S);
   if (one)
-    hipLaunchKernelGGL((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, true>), dim3(nblk), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, true>), dim3(nblk), dim3(64 * WM * WN), 0, st, p);
   else
-    hipLaunchKernelGGL((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, false>), dim3(nblk), dim3(64 * WM * WN), 0, st, p);
+    YV7_LAUNCH((conv_f16_ring_kernel<BM, BN, WM, WN, STAGES, false>), dim3(nblk), dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
 }
 

@@ -356,9 +356,9 @@ hipError_t launch_f8(const F8ConvParams& p, int occ, hipStream_t st) {
   const long cap = (long)cu_count() * occ;
   const int grid = (int)(T < cap ? T : cap);
   const dim3 blk(64 * WM * WN);
-  if (p.act == 1) hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 1, XF16>), dim3(grid), blk, 0, st, p);
-  else if (p.act == 2) hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 2, XF16>), dim3(grid), blk, 0, st, p);
-  else hipLaunchKernelGGL((conv_f8_kernel<BM, BN, WM, WN, STAGES, 0, XF16>), dim3(grid), blk, 0, st, p);
+  if (p.act == 1) YV7_LAUNCH((conv_f8_kernel<BM, BN, WM, WN, STAGES, 1, XF16>), dim3(grid), blk, 0, st, p);
+  else if (p.act == 2) YV7_LAUNCH((conv_f8_kernel<BM, BN, WM, WN, STAGES, 2, XF16>), dim3(grid), blk, 0, st, p);
+  else YV7_LAUNCH((conv_f8_kernel<BM, BN, WM, WN, STAGES, 0, XF16>), dim3(grid), blk, 0, st, p);
   return hipGetLastError();
 }
 
@@ -370,7 +370,7 @@ hipError_t launch_quant_f8(const void* x, int B, int H, int W, int xc, int xoff,
   const size_t work = (size_t)B * H * W * (kp / 16);
   size_t g = (work + 255) / 256;
   if (g > 256 * 16) g = 256 * 16;
-  hipLaunchKernelGGL(quant_f8_kernel, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st,
+  YV7_LAUNCH(quant_f8_kernel, dim3((unsigned)(g ? g : 1)), dim3(256), 0, st,
                      reinterpret_cast<const _Float16*>(x), B, H, W, xc, xoff, cin, kp, qscale,
                      reinterpret_cast<uint8_t*>(y8));
   return hipGetLastError();

@@ -207,7 +207,7 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_halo_kernel(const ConvParams p)
 template <int BN>
 hipError_t launch_bn(const ConvParams& p, hipStream_t st) {
   const int nblk = p.B * (p.Ho / TS) * (p.Wo / TS) * ((p.cout + BN - 1) / BN);
-  hipLaunchKernelGGL((conv3x3_halo_kernel<BN>), dim3(nblk), dim3(NT), 0, st, p);
+  YV7_LAUNCH((conv3x3_halo_kernel<BN>), dim3(nblk), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 

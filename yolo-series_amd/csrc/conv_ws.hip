@@ -290,14 +290,14 @@ hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st) {
   const int T = p.B * (p.H / TS) * (p.W / TS);
   const int grid = T < num_cus() ? T : num_cus();
   if (p.act == 1 && p.variant >= 17 && p.variant <= 19) {   // scheduling experiments (SiLU layers)
-    if (p.variant == 17) hipLaunchKernelGGL((conv3x3_ws64_kernel<1, 1>), dim3(grid), dim3(NT), 0, st, p);
-    else if (p.variant == 18) hipLaunchKernelGGL((conv3x3_ws64_kernel<1, 2>), dim3(grid), dim3(NT), 0, st, p);
-    else hipLaunchKernelGGL((conv3x3_ws64_kernel<1, 3>), dim3(grid), dim3(NT), 0, st, p);
+    if (p.variant == 17) YV7_LAUNCH((conv3x3_ws64_kernel<1, 1>), dim3(grid), dim3(NT), 0, st, p);
+    else if (p.variant == 18) YV7_LAUNCH((conv3x3_ws64_kernel<1, 2>), dim3(grid), dim3(NT), 0, st, p);
+    else YV7_LAUNCH((conv3x3_ws64_kernel<1, 3>), dim3(grid), dim3(NT), 0, st, p);
     return hipGetLastError();
   }
-  if (p.act == 1) hipLaunchKernelGGL((conv3x3_ws64_kernel<1>), dim3(grid), dim3(NT), 0, st, p);
-  else if (p.act == 2) hipLaunchKernelGGL((conv3x3_ws64_kernel<2>), dim3(grid), dim3(NT), 0, st, p);
-  else hipLaunchKernelGGL((conv3x3_ws64_kernel<0>), dim3(grid), dim3(NT), 0, st, p);
+  if (p.act == 1) YV7_LAUNCH((conv3x3_ws64_kernel<1>), dim3(grid), dim3(NT), 0, st, p);
+  else if (p.act == 2) YV7_LAUNCH((conv3x3_ws64_kernel<2>), dim3(grid), dim3(NT), 0, st, p);
+  else YV7_LAUNCH((conv3x3_ws64_kernel<0>), dim3(grid), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 

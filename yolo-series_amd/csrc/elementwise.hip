@@ -225,16 +225,16 @@ hipError_t input_t(const void* x, void* y, int B, int H, int W, int yc, bool reo
   const size_t npix = (size_t)B * (reorg ? (H / 2) * (W / 2) : H * W);
   if constexpr (std::is_same<T, _Float16>::value) {
     if (reorg && yc == 16) {
-      hipLaunchKernelGGL((input_reorg16_kernel<S>), dim3(grid_for(npix)), dim3(NT), 0, st, (const S*)x, (T*)y, B, H,
+      YV7_LAUNCH((input_reorg16_kernel<S>), dim3(grid_for(npix)), dim3(NT), 0, st, (const S*)x, (T*)y, B, H,
                          W);
       return hipGetLastError();
     }
   }
   if (reorg)
-    hipLaunchKernelGGL((input_kernel<T, S, true>), dim3(grid_for(npix)), dim3(NT), 0, st, (const S*)x, (T*)y, B, H,
+    YV7_LAUNCH((input_kernel<T, S, true>), dim3(grid_for(npix)), dim3(NT), 0, st, (const S*)x, (T*)y, B, H,
                        W, yc);
   else
-    hipLaunchKernelGGL((input_kernel<T, S, false>), dim3(grid_for(npix)), dim3(NT), 0, st, (const S*)x, (T*)y, B, H,
+    YV7_LAUNCH((input_kernel<T, S, false>), dim3(grid_for(npix)), dim3(NT), 0, st, (const S*)x, (T*)y, B, H,
                        W, yc);
   return hipGetLastError();
 }
@@ -254,10 +254,10 @@ hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc,
                           int yc, int yoff, int C, int k, int s, int pad, hipStream_t st) {
   const size_t work = (size_t)B * Ho * Wo * (C / (dtype == 1 ? 8 : 4));
   if (dtype == 1)
-    hipLaunchKernelGGL(maxpool_kernel<_Float16>, dim3(grid_for(work)), dim3(NT), 0, st, (const _Float16*)x, B, H, W,
+    YV7_LAUNCH(maxpool_kernel<_Float16>, dim3(grid_for(work)), dim3(NT), 0, st, (const _Float16*)x, B, H, W,
                        xc, xoff, (_Float16*)y, Ho, Wo, yc, yoff, C, k, s, pad);
   else
-    hipLaunchKernelGGL(maxpool_kernel<float>, dim3(grid_for(work)), dim3(NT), 0, st, (const float*)x, B, H, W, xc,
+    YV7_LAUNCH(maxpool_kernel<float>, dim3(grid_for(work)), dim3(NT), 0, st, (const float*)x, B, H, W, xc,
                        xoff, (float*)y, Ho, Wo, yc, yoff, C, k, s, pad);
   return hipGetLastError();
 }
@@ -266,10 +266,10 @@ hipError_t launch_upsample2x(int dtype, const void* x, int B, int H, int W, int 
                              int C, hipStream_t st) {
   const size_t work = (size_t)B * 4 * H * W * (C / (dtype == 1 ? 8 : 4));
   if (dtype == 1)
-    hipLaunchKernelGGL(upsample_kernel<_Float16>, dim3(grid_for(work)), dim3(NT), 0, st, (const _Float16*)x, B, H, W,
+    YV7_LAUNCH(upsample_kernel<_Float16>, dim3(grid_for(work)), dim3(NT), 0, st, (const _Float16*)x, B, H, W,
                        xc, xoff, (_Float16*)y, yc, yoff, C);
   else
-    hipLaunchKernelGGL(upsample_kernel<float>, dim3(grid_for(work)), dim3(NT), 0, st, (const float*)x, B, H, W, xc,
+    YV7_LAUNCH(upsample_kernel<float>, dim3(grid_for(work)), dim3(NT), 0, st, (const float*)x, B, H, W, xc,
                        xoff, (float*)y, yc, yoff, C);
   return hipGetLastError();
 }
@@ -278,10 +278,10 @@ hipError_t launch_copy(int dtype, const void* x, int B, int H, int W, int xc, in
                        int C, hipStream_t st) {
   const size_t work = (size_t)B * H * W * (C / (dtype == 1 ? 8 : 4));
   if (dtype == 1)
-    hipLaunchKernelGGL(copy_kernel<_Float16>, dim3(grid_for(work)), dim3(NT), 0, st, (const _Float16*)x, B, H, W, xc,
+    YV7_LAUNCH(copy_kernel<_Float16>, dim3(grid_for(work)), dim3(NT), 0, st, (const _Float16*)x, B, H, W, xc,
                        xoff, (_Float16*)y, yc, yoff, C);
   else
-    hipLaunchKernelGGL(copy_kernel<float>, dim3(grid_for(work)), dim3(NT), 0, st, (const float*)x, B, H, W, xc, xoff,
+    YV7_LAUNCH(copy_kernel<float>, dim3(grid_for(work)), dim3(NT), 0, st, (const float*)x, B, H, W, xc, xoff,
                        (float*)y, yc, yoff, C);
   return hipGetLastError();
 }
@@ -298,10 +298,10 @@ hipError_t launch_spp_cascade(int dtype, void* x, int B, int H, int W, int xc, i
   const size_t lds = (size_t)2 * H * W * (32 / V) * 16;
   const dim3 grid(B * (C / 32));
   if (dtype == 1)
-    hipLaunchKernelGGL(spp_cascade_kernel<_Float16>, grid, dim3(NT), lds, st, (const _Float16*)x, B, H, W, xc, coff, C,
+    YV7_LAUNCH(spp_cascade_kernel<_Float16>, grid, dim3(NT), lds, st, (const _Float16*)x, B, H, W, xc, coff, C,
                        (_Float16*)x);
   else
-    hipLaunchKernelGGL(spp_cascade_kernel<float>, grid, dim3(NT), lds, st, (const float*)x, B, H, W, xc, coff, C,
+    YV7_LAUNCH(spp_cascade_kernel<float>, grid, dim3(NT), lds, st, (const float*)x, B, H, W, xc, coff, C,
                        (float*)x);
   return hipGetLastError();
 }

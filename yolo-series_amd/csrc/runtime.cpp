@@ -50,7 +50,7 @@ struct yv7_plan {
   std::vector<WsKey> ws_ready;
   // per-op kernel variant override (0 = tuned dispatch; yv7_set_op_variant)
   std::vector<int> op_variant;
-  // live profiling: events[f * (n_ops + 1) + i]
+  // live profiling: events[f * 2 * n_ops + 2 * i + {0: start, 1: stop}] of op i in profiled forward f
   std::vector<hipEvent_t> events;
   int prof_max = 0, prof_used = 0;
 };
@@ -291,7 +291,7 @@ int yv7_profile_enable(yv7_plan* p, int max_forwards) {
   if (!p || max_forwards < 0) return fail(YV7_E_ARG, "yv7_profile_enable");
   free_events(p);
   if (max_forwards == 0) return 0;
-  const size_t n = (size_t)max_forwards * (p->ops.size() + 1);
+  const size_t n = (size_t)max_forwards * 2 * p->ops.size();
   p->events.resize(n);
   for (size_t i = 0; i < n; ++i) {
     hipError_t e = hipEventCreate(&p->events[i]);
@@ -311,12 +311,12 @@ int yv7_profile_read(yv7_plan* p, int* n_forwards, float* op_ms) {
   for (size_t i = 0; i < nops; ++i) op_ms[i] = 0.f;
   *n_forwards = p->prof_used;
   for (int f = 0; f < p->prof_used; ++f) {
-    hipEvent_t* ev = &p->events[(size_t)f * (nops + 1)];
-    hipError_t e = hipEventSynchronize(ev[nops]);
+    hipEvent_t* ev = &p->events[(size_t)f * 2 * nops];
+    hipError_t e = hipEventSynchronize(ev[2 * nops - 1]);
     if (e != hipSuccess) return hip_fail(e, "hipEventSynchronize");
     for (size_t i = 0; i < nops; ++i) {
       float ms = 0.f;
-      if ((e = hipEventElapsedTime(&ms, ev[i], ev[i + 1])) != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
+      if ((e = hipEventElapsedTime(&ms, ev[2 * i], ev[2 * i + 1])) != hipSuccess) return hip_fail(e, "hipEventElapsedTime");
       op_ms[i] += ms;
     }
   }
@@ -462,13 +462,18 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   const bool rowbest_fused = rowbest && yv7::det_writes_rowbest(p->dtype);
   hipEvent_t* ev = nullptr;
   if (p->prof_used < p->prof_max) {
-    ev = &p->events[(size_t)p->prof_used * (p->ops.size() + 1)];
+    ev = &p->events[(size_t)p->prof_used * 2 * p->ops.size()];
     p->prof_used++;
-    if ((e = hipEventRecord(ev[0], st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
   }
+  // the op's (start, stop) pair rides on its kernel launches (yv7_kernels.h YV7_LAUNCH); cleared on
+  // every way out of this function
+  struct EventScope {
+    ~EventScope() { yv7::op_events() = yv7::OpEvents{}; }
+  } event_scope;
   size_t fused_until = 0;   // ops [.., fused_until) were launched as part of a fused group
   for (size_t i = 0; i < p->ops.size(); ++i) {
     const auto& o = p->ops[i];
+    if (ev) yv7::op_events() = yv7::OpEvents{ev[2 * i], ev[2 * i + 1], 0};
     switch (o.kind) {
       case YV7_OP_INPUT: {
         const auto& t = p->tensors[o.dst];
@@ -624,8 +629,12 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
         return fail(YV7_E_ARG, "yv7_forward: unknown op kind");
     }
     if (e != hipSuccess) return hip_fail(e, "yv7_forward launch");
-    if (ev && (e = hipEventRecord(ev[i + 1], st)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    if (ev && yv7::op_events().launches == 0) {   // no kernel of its own (a later op of a fused cascade)
+      if ((e = hipEventRecord(ev[2 * i], st)) != hipSuccess || (e = hipEventRecord(ev[2 * i + 1], st)) != hipSuccess)
+        return hip_fail(e, "hipEventRecord");
+    }
   }
+  yv7::op_events() = yv7::OpEvents{};
   if (rowbest && !rowbest_fused &&
       (e = yv7::launch_row_best(z, B, nrows, p->no, rowbest, st)) != hipSuccess)
     return hip_fail(e, "yv7_forward row scores");

@@ -281,7 +281,7 @@ hipError_t stem_t(const StemParams& p, hipStream_t st) {
   }();
   static const int occ = [] { const char* e = getenv("YV7_STEM_OCC"); return e ? atoi(e) : 2; }();
   const int nblk = ntiles < cus * occ ? ntiles : cus * occ;   // persistent: blocks walk the tiles
-  hipLaunchKernelGGL((stem_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B>), dim3(nblk), dim3(NT), 0, st, p);
+  YV7_LAUNCH((stem_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B>), dim3(nblk), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 

@@ -1,11 +1,34 @@
 // Shared definitions of the yv7 HIP kernels (gfx950 / CDNA4 only).
 #pragma once
+#include <hip/hip_ext.h>
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include <type_traits>
 
 namespace yv7 {
+
+// Live per-op kernel timing (runtime.cpp's profile mode).  While a forward is profiled the runtime
+// points op_events() at the current op's (start, stop) event pair, and every kernel of the op is
+// launched through hipExtLaunchKernel with the first launch carrying `start` and each launch `stop`:
+// the pair then spans the op's own dispatches (the begin / end timestamps rocprofv3's kernel trace
+// reports), not the interval between two markers on the stream, which with batches in flight also
+// counts the time a kernel waits for CUs the other streams' kernels hold.  Null events: a plain launch.
+struct OpEvents {
+  hipEvent_t start = nullptr, stop = nullptr;
+  int launches = 0;
+};
+inline OpEvents& op_events() {
+  static thread_local OpEvents e;
+  return e;
+}
+#define YV7_LAUNCH(kernel, grid, block, shmem, st, ...)                                                    \
+  do {                                                                                                     \
+    ::yv7::OpEvents& ev_ = ::yv7::op_events();                                                             \
+    hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, ev_.launches ? nullptr : ev_.start, ev_.stop, 0, \
+                          __VA_ARGS__);                                                                    \
+    if (ev_.stop) ev_.launches++;                                                                          \
+  } while (0)
 
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef float f4 __attribute__((ext_vector_type(4)));
