@@ -19,8 +19,7 @@ NMS = ('nms_compact', 'nms_fast', 'nms_rows', 'nms_scan', 'nms_write', 'nms_sort
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r['Dispatch_Id']))
 bench = json.load(open(sys.argv[2]))
 warm, steps = bench['warmup'], bench['steps']
-live = bench['roofline'].get('timing', '')
-nlive = int(live.split(' of ')[1].split()[0]) if ' of ' in live else 0
+nlive = int(bench.get('detail', {}).get('profiled_forwards') or 0)
 fwd = -1
 per = {}
 for r in rows:

@@ -1953,6 +1953,15 @@ hipError_t launch_p8w(const ConvParams& p, bool one, hipStream_t st) {
   return hipGetLastError();
 }
 
+// 128-channel 3x3 stride-1 layers with at least one round of 512 x 128 tiles on the 8-phase ring
+// (variant 238) — YV7_P8W=1 (bench A/B under batches in flight: alone on the chip it ties the 2-phase
+// ring, the last partial round of its 400 tiles leaving CUs idle that other streams can fill).
+bool p8w_default(const ConvParams& p) {
+  static const int on = [] { const char* e = getenv("YV7_P8W"); return e ? atoi(e) : 0; }();
+  return on && !p.pool && p.k == 3 && p.s == 1 && p.cout == 128 && p.cin >= 128 && p.cin % BKE == 0 &&
+         p.yoff % 8 == 0 && p.yc % 8 == 0 && (long)((p.M + 511) / 512) >= device_cus();
+}
+
 hipError_t launch_p8n(const ConvParams& p, bool one, hipStream_t st) {
   if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || (!one && p.cin % BKE)) return hipErrorInvalidValue;
   const long T = (long)((p.M + 255) / 256) * ((p.cout + 127) / 128);
@@ -2164,6 +2173,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
       if (p.K <= 512 && p.M >= 51200) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     } else if (wide && p.k == 3 && p.cin >= 256 && p.cout >= 256 && t256 >= 200) {
       return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
+    } else if (p8w_default(p)) {
+      return launch_p8w(p, false, st);
     } else if (p.k == 3 && p.cout == 128) {
       // (3x3 512->512 @20 and s2 from @40 take the non-persistent 128 x 128 ring of choose() below:
       // in-network 92 (this ring) / 89 (256 x 128 persistent) -> 79 us; with fewer tiles than CUs,
