@@ -267,6 +267,274 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
   }
 }
 
+// Second form (the default; YV7_STEM=1 selects the kernel above).  Same tile, same arithmetic bit for
+// bit, restructured after its microbenchmark hooks (scripts/stembench.hip: conv B's 72 ds_read_b128
+// per wave per tile cost as much as its MFMAs, the two not overlapping; 5 barriers per tile):
+//   * conv B: wave w owns 4 m-tiles x 2 n-tiles (32 output channels, 18 weight fragments in registers)
+//     instead of 8 m-tiles x 16 channels: half the LDS reads of conv A's tile for the same MFMAs;
+//   * conv A: m-tiles in groups of three (12 MFMAs issued back to back, then their activations);
+//   * the output staging tile has its own LDS (patch + A tile + staging = 68.6 KB, two blocks per CU),
+//     so a tile needs 3 barriers: [stores of t-1, patch of t] | conv A | conv B + staging;
+//   * both biases in registers from kernel entry (no global load inside the tile loop).
+template <typename S, int CA, int CB, int SA, int TBY, int TBX, int ACT_A, int ACT_B>
+__global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
+  constexpr int TAY = 2 * TBY + 1, TAX = 2 * TBX + 1;
+  constexpr int PY = SA * (TAY - 1) + 3, PX = SA * (TAX - 1) + 3;
+  constexpr int NA = TAY * TAX;
+  constexpr int MA = (NA + 15) / 16;
+  constexpr int APITCH = CA * 2 + 16;
+  constexpr int PATCH = (PY * PX * 8 + 15) / 16 * 16;
+  constexpr int ABUF = (NA * APITCH + 15) / 16 * 16;
+  constexpr int MB = TBY * TBX / 16;
+  constexpr int CPITCH = CB * 2 + 16;
+  constexpr int OUTB = TBY * TBX * CPITCH;
+  static_assert(CB == 64 && CA == 32, "4 waves = 2 m-groups x 2 n-groups of 32 channels; one MFMA k-step per tap");
+  static_assert(MB == 8 && MA % 12 == 0, "conv B: 4 m-tiles per wave; conv A: groups of 3 m-tiles per wave");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[PATCH + ABUF + OUTB];
+  _Float16* patch = reinterpret_cast<_Float16*>(smem);
+  unsigned char* abuf = smem + PATCH;
+  unsigned char* obuf = smem + PATCH + ABUF;
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, li = lane & 15;
+  const int mg = wave >> 1, ng = wave & 1;        // conv B: m-tiles [4 mg, 4 mg + 4), channels [32 ng, 32 ng + 32)
+  const int HA = p.H / SA, WA = p.W / SA;
+  const int HB = HA / 2, WB = WA / 2;
+  const int tiles_x = (WB + TBX - 1) / TBX, tiles_y = (HB + TBY - 1) / TBY;
+  const int ntiles = p.B * tiles_x * tiles_y;
+  auto tile_geom = [&](int t, int& tb, int& ty, int& tx) {
+    tb = t / (tiles_x * tiles_y);
+    t -= tb * tiles_x * tiles_y;
+    ty = (t / tiles_x) * TBY;
+    tx = (t % tiles_x) * TBX;
+  };
+  constexpr float NLOG2E = -1.4426950408889634f;
+  const float sa_scale = ACT_A == 1 ? NLOG2E : 1.0f;
+  const float sb_scale = ACT_A == 1 ? NLOG2E : 1.0f;
+
+  // conv-B weight fragments: this wave's 2 n-tiles x 9 taps
+  u4 wfr[2][9];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int tap = 0; tap < 9; ++tap)
+      wfr[j][tap] = *reinterpret_cast<const u4*>(reinterpret_cast<const _Float16*>(p.wb) +
+                                                 (size_t)((2 * ng + j) * 16 + li) * p.kpad_b + tap * CA + g * 8);
+  float bb_l[2][4];
+#pragma unroll
+  for (int j = 0; j < 2; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bb_l[j][e] = p.bb[(2 * ng + j) * 16 + g * 4 + e] * sb_scale;
+
+  constexpr int PPT = (PY * PX + NT - 1) / NT;
+  S pre[PPT][3];
+  auto prefetch = [&](int t) {
+    int tb, ty, tx;
+    tile_geom(t, tb, ty, tx);
+    const int iy0 = SA * (2 * ty - 1) - 1, ix0 = SA * (2 * tx - 1) - 1;
+    const S* xb = reinterpret_cast<const S*>(p.x) + (size_t)tb * 3 * p.H * p.W;
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int i = tid + k * NT;
+      const int py = i / PX, px = i - py * PX;
+      const int iy = iy0 + py, ix = ix0 + px;
+      pre[k][0] = pre[k][1] = pre[k][2] = (S)0.f;
+      if (i < PY * PX && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2) {
+        const size_t o = (size_t)iy * p.W + ix;
+        pre[k][0] = xb[o];
+        pre[k][1] = xb[o + (size_t)p.H * p.W];
+        pre[k][2] = xb[o + 2 * (size_t)p.H * p.W];
+      }
+    }
+  };
+  auto commit = [&]() {
+#pragma unroll
+    for (int k = 0; k < PPT; ++k) {
+      const int i = tid + k * NT;
+      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+      const h4 v = {(_Float16)(float)pre[k][0], (_Float16)(float)pre[k][1], (_Float16)(float)pre[k][2],
+                    (_Float16)0.f};
+      if (i < PY * PX) *reinterpret_cast<h4*>(patch + i * 4) = v;
+    }
+  };
+  // conv A's K layout (as stem_kernel): two taps per 8-half lane group
+  auto tap_of = [](int ks, int gg, int half) -> int {
+    if (ks == 0) {
+      if (gg < 3) return gg * 3 + half;
+      return half == 0 ? 2 : 5;
+    }
+    return (gg == 0 && half == 0) ? 8 : -1;
+  };
+  constexpr int NAT = CA / 16;
+  u4 wa[2][NAT];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int nt = 0; nt < NAT; ++nt) {
+      typedef _Float16 h8v __attribute__((ext_vector_type(8)));
+      h8v w8;
+      const _Float16* wrow = reinterpret_cast<const _Float16*>(p.wa) + (size_t)(nt * 16 + li) * p.kpad_a;
+#pragma unroll
+      for (int h2 = 0; h2 < 2; ++h2) {
+        const int tap = tap_of(ks, g, h2);
+#pragma unroll
+        for (int ci = 0; ci < 4; ++ci)
+          w8[h2 * 4 + ci] = (tap >= 0 && ci < 3) ? (_Float16)((float)wrow[tap * 3 + ci] * sa_scale) : (_Float16)0.f;
+      }
+      wa[ks][nt] = __builtin_bit_cast(u4, w8);
+    }
+  int toff[2][2];
+#pragma unroll
+  for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+    for (int h2 = 0; h2 < 2; ++h2) {
+      const int tap = tap_of(ks, g, h2);
+      toff[ks][h2] = tap >= 0 ? ((tap / 3) * PX + tap % 3) * 8 : -1;
+    }
+  float ba_l[NAT][4];
+#pragma unroll
+  for (int nt = 0; nt < NAT; ++nt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ba_l[nt][e] = p.ba[nt * 16 + g * 4 + e] * sa_scale;
+
+  const int G = gridDim.x;
+  const int vb = G % 8 == 0 ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  if (vb < ntiles) prefetch(vb);
+  int pb = -1, poy0 = 0, pox0 = 0;   // the previous tile (its staged output is stored in this iteration)
+  auto store_prev = [&]() {
+    if (pb < 0) return;
+    constexpr int CPR = CB * 2 / 16;
+    _Float16* y = reinterpret_cast<_Float16*>(p.y);
+#pragma unroll
+    for (int k = 0; k < TBY * TBX * CPR / NT; ++k) {
+      const int c = tid + k * NT;
+      const int mb = c / CPR, ch = c - mb * CPR;
+      const int ty = mb / TBX, tx = mb - ty * TBX;
+      const int oy = poy0 + ty, ox = pox0 + tx;
+      if (oy < HB && ox < WB && p.variant != 4)
+        *reinterpret_cast<u4*>(y + pix_index(pb, oy, ox, HB, WB) * p.yc + p.yoff + ch * 8) =
+            *reinterpret_cast<const u4*>(obuf + mb * CPITCH + ch * 16);
+    }
+  };
+  for (int tile = vb; tile < ntiles; tile += G) {
+    int b, oy0, ox0;
+    tile_geom(tile, b, oy0, ox0);
+    const int ay0 = 2 * oy0 - 1, ax0 = 2 * ox0 - 1;
+    commit();
+    if (tile + G < ntiles) prefetch(tile + G);
+    store_prev();
+    __syncthreads();   // patch of this tile in LDS; staging of the previous one read
+
+    // conv A -> abuf, three m-tiles per group
+    {
+      const unsigned char* pbytes = reinterpret_cast<const unsigned char*>(patch);
+      typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+#pragma unroll 1
+      for (int grp = 0; grp < MA / 12; ++grp) {
+        u4 xv[3][2];
+        int mm[3];
+        bool inside[3];
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+          const int m = (grp * 3 + u) * 4 * 16 + wave * 16 + li;   // m-tile (grp*3+u)*4 + wave
+          mm[u] = m;
+          const int mc = m < NA ? m : NA - 1;
+          const int yl = mc / TAX, xl = mc - yl * TAX;
+          const int base = (SA * yl * PX + SA * xl) * 8;
+#pragma unroll
+          for (int ks = 0; ks < 2; ++ks) {
+            u2 lo = {0u, 0u}, hi = {0u, 0u};
+            if (toff[ks][0] >= 0) lo = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][0]);
+            if (toff[ks][1] >= 0) hi = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][1]);
+            xv[u][ks] = u4{lo[0], lo[1], hi[0], hi[1]};
+          }
+          const int ay = ay0 + yl, ax = ax0 + xl;
+          inside[u] = m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA;
+        }
+        f4 acc[3][NAT];
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+          for (int nt = 0; nt < NAT; ++nt) {
+            f4 a = {ba_l[nt][0], ba_l[nt][1], ba_l[nt][2], ba_l[nt][3]};
+            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[0][nt]), __builtin_bit_cast(h8, xv[u][0]),
+                                                       a, 0, 0, 0);
+            acc[u][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[1][nt]),
+                                                                __builtin_bit_cast(h8, xv[u][1]), a, 0, 0, 0);
+          }
+#pragma unroll
+        for (int u = 0; u < 3; ++u)
+#pragma unroll
+          for (int nt = 0; nt < NAT; ++nt) {
+            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+            h4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              float v;
+              if (p.variant == 1) v = acc[u][nt][e];
+              else if constexpr (ACT_A == 1) v = acc[u][nt][e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[u][nt][e]));
+              else v = act_t<ACT_A>(acc[u][nt][e]);
+              o[e] = inside[u] ? (_Float16)v : (_Float16)0.f;
+            }
+            if (mm[u] < NA) *reinterpret_cast<h4*>(abuf + mm[u] * APITCH + (nt * 16 + g * 4) * 2) = o;
+          }
+      }
+    }
+    __syncthreads();   // A tile complete
+
+    // conv B: 4 m-tiles x 2 n-tiles per wave, then activation -> staging
+    f4 acc[4][2];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) acc[i][j] = f4{bb_l[j][0], bb_l[j][1], bb_l[j][2], bb_l[j][3]};
+    if (p.variant != 3) {
+#pragma unroll
+      for (int tap = 0; tap < 9; ++tap) {
+        const int r = tap / 3, s = tap - r * 3;
+        u4 xa[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          const int mb = (4 * mg + i) * 16 + li;
+          const int ty = mb / TBX, tx = mb - ty * TBX;
+          const int ap = (2 * ty + r) * TAX + (2 * tx + s);
+          xa[i] = *reinterpret_cast<const u4*>(abuf + ap * APITCH + g * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wfr[j][tap]),
+                                                               __builtin_bit_cast(h8, xa[i]), acc[i][j], 0, 0, 0);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const int mb = (4 * mg + i) * 16 + li;
+        const int col = (2 * ng + j) * 16 + g * 4;
+        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+        h4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float v;
+          if constexpr (ACT_A == 1 && ACT_B == 1)
+            v = (acc[i][j][e] * -0.6931471805599453f) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[i][j][e]));
+          else
+            v = act_t<ACT_B>(acc[i][j][e] / sb_scale);
+          o[e] = (_Float16)v;
+        }
+        *reinterpret_cast<h4*>(obuf + mb * CPITCH + col * 2) = o;
+      }
+    pb = b;
+    poy0 = oy0;
+    pox0 = ox0;
+    __syncthreads();   // staging complete (stored at the top of the next iteration)
+  }
+  store_prev();
+}
+
 template <typename S, int CA, int CB, int SA, int ACT_A, int ACT_B>
 hipError_t stem_t(const StemParams& p, hipStream_t st) {
   constexpr int TBY = 8, TBX = 16;
@@ -281,6 +549,13 @@ hipError_t stem_t(const StemParams& p, hipStream_t st) {
   }();
   static const int occ = [] { const char* e = getenv("YV7_STEM_OCC"); return e ? atoi(e) : 2; }();
   const int nblk = ntiles < cus * occ ? ntiles : cus * occ;   // persistent: blocks walk the tiles
+  static const int form = [] { const char* e = getenv("YV7_STEM"); return e ? atoi(e) : 2; }();
+  if constexpr (SA == 1) {   // (SA = 2, yolov7-tiny: its 10 patch pixels per thread leave stem2 one block per CU)
+    if (form != 1) {
+      YV7_LAUNCH((stem2_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B>), dim3(nblk), dim3(NT), 0, st, p);
+      return hipGetLastError();
+    }
+  }
   YV7_LAUNCH((stem_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B>), dim3(nblk), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
