@@ -227,12 +227,15 @@ def main(argv=None):
     local = int(os.environ.get('LOCAL_RANK', '0'))
     if world != a.gpus:
         raise SystemExit(f'--gpus {a.gpus} but WORLD_SIZE={world}')
-    distributed = world > 1
+    # YV7_BENCH_DIST=1 takes the multi-rank path (RCCL broadcast + per-batch all-gather) even with one
+    # rank, so the RCCL data path can be exercised on a one-GPU box
+    force_dist = os.environ.get('YV7_BENCH_DIST') == '1'
+    distributed = world > 1 or force_dist
+    torch.cuda.set_device(local)
     if distributed:
         dist.init_process_group('nccl', device_id=torch.device(f'cuda:{local}'))
         if dist.get_world_size() != a.gpus:
             raise SystemExit(f'--gpus {a.gpus} but RCCL sees {dist.get_world_size()} ranks')
-    torch.cuda.set_device(local)
     dev = torch.device(f'cuda:{local}')
 
     from models.yolo import Model
@@ -278,7 +281,8 @@ def main(argv=None):
     if nstreams > 1:   # yv7.runtime.Inflight: the library's serving schedule, S batches in flight
         from yv7.runtime import Inflight
         prios = [int(v) for v in a.prio.split(',')] if a.prio else None
-        runner = Inflight(plan, B, H, W, streams=nstreams, post=ydist.gather_detections if distributed else None,
+        gather = (lambda d, s_, c: ydist.gather_detections(d, s_, c, force=force_dist)) if distributed else None
+        runner = Inflight(plan, B, H, W, streams=nstreams, post=gather,
                           priorities=prios)
     zs = [torch.empty((B, N, plan.no), dtype=torch.float32, device=dev) for _ in range(nbuf)]
     dets = [torch.empty((B, 300, 6), dtype=torch.float32, device=dev) for _ in range(nbuf)]
@@ -313,7 +317,7 @@ def main(argv=None):
     def post(k):
         nms_batched(zs[k], 0.25, 0.45, out=(dets[k], srcs[k], cnts[k]), rowbest=rowbests[k])
         if distributed:
-            ydist.gather_detections(dets[k], srcs[k], cnts[k])
+            ydist.gather_detections(dets[k], srcs[k], cnts[k], force=force_dist)
 
     def step():
         k = nstep[0] % nbuf

@@ -93,3 +93,41 @@ def test_bench_launcher_starts_ranks():
     assert len(lines) == 1, out.stdout
     r = lines[0]
     assert r['n_gpus'] == 2 and r['world_size_seen'] == 2 and r['all_ranks_ok'] and r['global_batch'] == 6
+
+
+@pytest.mark.gpu
+def test_rccl_world1_broadcast_gather_inflight():
+    """The RCCL data path on one MI355X (world size 1, the collectives issued anyway): the weight blob
+    broadcast, then three batches in flight on three streams each all-gathering its detections from
+    its own stream (yv7.runtime.Inflight post=) — the results equal a serial run's (the per-batch
+    all-gather the 8-GPU bench issues, on the real backend)."""
+    from functools import partial
+
+    from helpers import fresh_model, frames
+    from utils.general import nms_batched
+    from yv7.dist import broadcast_weights
+    from yv7.runtime import Inflight
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()))
+    dev = torch.device('cuda:0')
+    torch.cuda.set_device(dev)
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
+    try:
+        plan = broadcast_weights(fresh_model('yolov7-tiny'), dev, torch.float16)
+        B, H, W = 4, 256, 320
+        xs = [frames(B, H, W, seed=70 + i).to(dev).half() for i in range(4)]
+        ref = []
+        for x in xs:
+            z = torch.empty((B, plan.num_rows(H, W), plan.no), dtype=torch.float32, device=dev)
+            plan.forward_into(x, z)
+            ref.append(nms_batched(z, 0.25, 0.45))
+        run = Inflight(plan, B, H, W, streams=3, post=partial(gather_detections, force=True))
+        hs = [run.submit(x) for x in xs]
+        for h, (det, src, cnt) in zip(hs[1:], ref[1:]):
+            gd, gs, gc = run.result(h)
+            assert gd.shape == det.shape and torch.equal(gc, cnt)
+            for b in range(B):
+                n = int(cnt[b])
+                assert torch.equal(gd[b, :n], det[b, :n]) and torch.equal(gs[b, :n], src[b, :n])
+        run.close()
+    finally:
+        dist.destroy_process_group()

@@ -46,10 +46,12 @@ def broadcast_weights(model, device, dtype, group=None):
     return Plan(g, device, broadcast_blob(g, device, group))
 
 
-def gather_detections(det, src_row, count, group=None):
-    """All-gather fixed-shape per-rank NMS outputs -> global (det, src_row, count) in image order."""
+def gather_detections(det, src_row, count, group=None, force=False):
+    """All-gather fixed-shape per-rank NMS outputs -> global (det, src_row, count) in image order.
+    One rank: the inputs themselves, unless force (the collective is then issued anyway — a one-GPU
+    check of the RCCL path)."""
     world = dist.get_world_size(group)
-    if world == 1:
+    if world == 1 and not force:
         return det, src_row, count
     outs = []
     for t in (det, src_row, count):
