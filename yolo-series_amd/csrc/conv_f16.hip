@@ -591,7 +591,7 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
 // channels [w BN/4, (w+1) BN/4) of all BMP rows.  The epilogue stages both tiles in LDS and stores
 // 16-byte chunks, as conv_f16_kernel does.  Same K order and bias-initialised accumulators as the
 // two separate kernels.
-template <int BMP, int BN, int OCC, int PF>
+template <int BMP, int BN, int OCC>
 __global__ __launch_bounds__(NT, OCC) void conv_f16_twin_kernel(const ConvParams p, const ConvParams q) {
   static_assert(BMP == 32 && BN % 64 == 0, "one pooled row per thread and K chunk");
   constexpr int BMU = 4 * BMP;                    // plain-conv rows
@@ -727,30 +727,12 @@ __global__ __launch_bounds__(NT, OCC) void conv_f16_twin_kernel(const ConvParams
   u4 ra[4], rp[RB], rq[RB];
   gload(0, ra, rp, rq);
   lstore(0, ra, rp, rq);
-  if constexpr (PF == 1) {
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    if (kt + 1 < nk) gload(kt + 1, ra, rp, rq);
+    compute(kt & 1);
+    if (kt + 1 < nk) lstore((kt & 1) ^ 1, ra, rp, rq);
     __syncthreads();
-    for (int kt = 0; kt < nk; ++kt) {
-      if (kt + 1 < nk) gload(kt + 1, ra, rp, rq);
-      compute(kt & 1);
-      if (kt + 1 < nk) lstore((kt & 1) ^ 1, ra, rp, rq);
-      __syncthreads();
-    }
-  } else {
-    // two register sets: step kt+2's loads are issued before step kt's MFMAs (two steps to land)
-    u4 ra2[4], rp2[RB], rq2[RB];
-    if (nk > 1) gload(1, ra2, rp2, rq2);
-    __syncthreads();
-    for (int kt = 0; kt < nk; kt += 2) {
-      if (kt + 2 < nk) gload(kt + 2, ra, rp, rq);
-      compute(0);
-      if (kt + 1 < nk) lstore(1, ra2, rp2, rq2);
-      __syncthreads();
-      if (kt + 1 >= nk) break;
-      if (kt + 3 < nk) gload(kt + 3, ra2, rp2, rq2);
-      compute(1);
-      if (kt + 2 < nk) lstore(0, ra, rp, rq);
-      __syncthreads();
-    }
   }
 
   // epilogue: one staged tile, plain rows [0, BMU) then pooled rows [BMU, BMU + BMP)
@@ -2502,8 +2484,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
 }
 
 // MP twin (conv_f16_twin_kernel): the pooled 1x1 conv p and the plain 1x1 conv q of one MP block,
-// one launch.  YV7_TWIN: 1 (default) BN 64, two blocks per CU, loads two K steps ahead; 2 BN 128, one
-// block per CU; 3 BN 64, one step ahead; 0 off.
+// one launch.  YV7_TWIN: 1 (default) BN 64 with two blocks per CU, 2 BN 128 with one, 0 off.
 int twin_form() {
   static const int f = [] { const char* e = getenv("YV7_TWIN"); return e ? atoi(e) : 1; }();
   return f;
@@ -2521,13 +2502,10 @@ hipError_t launch_conv_twin_f16(const ConvParams& p, const ConvParams& q, hipStr
   if (!twin_supported(p, q)) return hipErrorInvalidValue;
   constexpr int BMP = 32;
   const int nM = (p.M + BMP - 1) / BMP;
-  const int f = twin_form();
-  if (f == 2) {
-    YV7_LAUNCH((conv_f16_twin_kernel<BMP, 128, 1, 2>), dim3(nM * ((p.cout + 127) / 128)), dim3(NT), 0, st, p, q);
-  } else if (f == 3) {
-    YV7_LAUNCH((conv_f16_twin_kernel<BMP, 64, 2, 1>), dim3(nM * ((p.cout + 63) / 64)), dim3(NT), 0, st, p, q);
+  if (twin_form() == 2) {
+    YV7_LAUNCH((conv_f16_twin_kernel<BMP, 128, 1>), dim3(nM * ((p.cout + 127) / 128)), dim3(NT), 0, st, p, q);
   } else {
-    YV7_LAUNCH((conv_f16_twin_kernel<BMP, 64, 2, 2>), dim3(nM * ((p.cout + 63) / 64)), dim3(NT), 0, st, p, q);
+    YV7_LAUNCH((conv_f16_twin_kernel<BMP, 64, 2>), dim3(nM * ((p.cout + 63) / 64)), dim3(NT), 0, st, p, q);
   }
   return hipGetLastError();
 }
