@@ -578,217 +578,6 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
 }
 
 
-// MP twin.  yolov7's MP block reads one tensor twice: MP -> Conv 1x1 (here a 1x1 conv with the 2x2
-// max folded into its operand loads, ConvParams::pool) and Conv 1x1 on the same tensor
-// (cfg/deploy/yolov7.yaml:27-29 and :40-42, the head's MP blocks; models/common.py:110-111 after the
-// MP of common.py:30-37).  One launch computes both from a single read of the input: a block owns BMP
-// pooled pixels and BN output channels of both convs; its threads load each pooled pixel's four
-// window pixels (16 bytes per K chunk each), write them as the four A rows of the plain conv (window
-// position w = 2 dy + dx -> rows [w BMP, (w+1) BMP)) and their max as the A row of the pooled conv.
-//   p: the pooled conv (pool = 2, k = 1, s = 2; output Ho x Wo), q: the plain 1x1 conv (output
-//   2 Ho x 2 Wo); same input slice, cin, cout and activation (twin_supported).
-// Waves: wave w computes the plain conv's window-position-w rows (BMP x BN) and the pooled conv's
-// channels [w BN/4, (w+1) BN/4) of all BMP rows.  The epilogue stages both tiles in LDS and stores
-// 16-byte chunks, as conv_f16_kernel does.  Same K order and bias-initialised accumulators as the
-// two separate kernels.
-template <int BMP, int BN, int OCC>
-__global__ __launch_bounds__(NT, OCC) void conv_f16_twin_kernel(const ConvParams p, const ConvParams q) {
-  static_assert(BMP == 32 && BN % 64 == 0, "one pooled row per thread and K chunk");
-  constexpr int BMU = 4 * BMP;                    // plain-conv rows
-  constexpr int RB = BN / 32;                     // weight rows per thread, per conv
-  constexpr int TMU = BMP / 16, TNU = BN / 16;    // plain conv: wave tile BMP x BN
-  constexpr int TMP = BMP / 16, TNP = BN / 64;    // pooled conv: wave tile BMP x BN/4
-  constexpr int STAGE = (BMU + BMP + 2 * BN) * ROWB;
-  constexpr int CPITCH = BN * 2 + 16;
-  constexpr int EPI = (BMU + BMP) * (CPITCH + 4);
-  constexpr int LDS = (2 * STAGE > EPI) ? 2 * STAGE : EPI;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int g = lane >> 4, li = lane & 15;
-  const int nwg = gridDim.x, bid = blockIdx.x;
-  const int qq = nwg >> 3, rr = nwg & 7, xcd = bid & 7, loc = bid >> 3;
-  const int wgid = (xcd < rr ? xcd * (qq + 1) : rr * (qq + 1) + (xcd - rr) * qq) + loc;
-  const int nN = (p.cout + BN - 1) / BN;
-  const int m0 = (wgid / nN) * BMP, n0 = (wgid % nN) * BN;
-
-  const auto xr = make_rsrc(p.x, p.xbytes);
-  const auto wpr = make_rsrc(p.w, p.wbytes);
-  const auto wqr = make_rsrc(q.w, q.wbytes);
-  const int c = tid & 7, r0 = tid >> 3;
-  uint32_t aoff;
-  {
-    PixelWalk pw(p, m0 + r0);   // rows past M walk into image B: offsets beyond the input (zeros)
-    aoff = a_origin(p, pw.b, pw.ho, pw.wo, c);
-  }
-  uint32_t b_off[RB];
-#pragma unroll
-  for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)(((n0 + r0 + 32 * j) * p.kpad + c * 8) * 2);
-  const int nk = p.kpad / BKE;
-  const uint32_t pdx = (uint32_t)p.xc * 2, pdy = (uint32_t)(p.W + 2 * BORDER) * p.xc * 2;
-
-  auto gload = [&](int kt, u4 (&ra)[4], u4 (&rp)[RB], u4 (&rq)[RB]) {
-    const uint32_t so = (uint32_t)kt * BKE * 2;
-    ra[0] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, aoff, so, 0));
-    ra[1] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, aoff + pdx, so, 0));
-    ra[2] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, aoff + pdy, so, 0));
-    ra[3] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, aoff + pdy + pdx, so, 0));
-#pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      rp[j] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(wpr, b_off[j], so, 0));
-      rq[j] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(wqr, b_off[j], so, 0));
-    }
-  };
-  // stage layout: [plain A: BMU rows][pooled A: BMP rows][pooled W: BN rows][plain W: BN rows]
-  auto lstore = [&](int buf, const u4 (&ra)[4], const u4 (&rp)[RB], const u4 (&rq)[RB]) {
-    unsigned char* Au = smem + buf * STAGE;
-    unsigned char* Ap = Au + BMU * ROWB;
-    unsigned char* Bp = Ap + BMP * ROWB;
-    unsigned char* Bq = Bp + BN * ROWB;
-#pragma unroll
-    for (int w = 0; w < 4; ++w) {
-      const int row = w * BMP + r0;
-      *reinterpret_cast<u4*>(Au + row * ROWB + swz(row, c) * 16) = ra[w];
-    }
-    *reinterpret_cast<u4*>(Ap + r0 * ROWB + swz(r0, c) * 16) = hmax4(ra[0], ra[1], ra[2], ra[3]);
-#pragma unroll
-    for (int j = 0; j < RB; ++j) {
-      const int row = r0 + 32 * j;
-      *reinterpret_cast<u4*>(Bp + row * ROWB + swz(row, c) * 16) = rp[j];
-      *reinterpret_cast<u4*>(Bq + row * ROWB + swz(row, c) * 16) = rq[j];
-    }
-  };
-
-  f4 accq[TNU][TMU], accp[TNP][TMP];
-#pragma unroll
-  for (int j = 0; j < TNU; ++j) {
-    const int col = n0 + j * 16 + g * 4;
-    f4 bv;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bv[e] = col + e < q.cout ? q.bias[col + e] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TMU; ++i) accq[j][i] = bv;
-  }
-#pragma unroll
-  for (int j = 0; j < TNP; ++j) {
-    const int col = n0 + wave * (BN / 4) + j * 16 + g * 4;
-    f4 bv;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TMP; ++i) accp[j][i] = bv;
-  }
-
-  auto compute = [&](int buf) {
-    const unsigned char* Au = smem + buf * STAGE;
-    const unsigned char* Ap = Au + BMU * ROWB;
-    const unsigned char* Bp = Ap + BMP * ROWB;
-    const unsigned char* Bq = Bp + BN * ROWB;
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const int ch = s * 4 + g;
-      u4 xu[TMU], xp[TMP], wq[TNU], wp[TNP];
-#pragma unroll
-      for (int i = 0; i < TMU; ++i) {
-        const int row = wave * BMP + i * 16 + li;
-        xu[i] = *reinterpret_cast<const u4*>(Au + row * ROWB + swz(row, ch) * 16);
-      }
-#pragma unroll
-      for (int i = 0; i < TMP; ++i) {
-        const int row = i * 16 + li;
-        xp[i] = *reinterpret_cast<const u4*>(Ap + row * ROWB + swz(row, ch) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < TNU; ++j) {
-        const int row = j * 16 + li;
-        wq[j] = *reinterpret_cast<const u4*>(Bq + row * ROWB + swz(row, ch) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < TNP; ++j) {
-        const int row = wave * (BN / 4) + j * 16 + li;
-        wp[j] = *reinterpret_cast<const u4*>(Bp + row * ROWB + swz(row, ch) * 16);
-      }
-#pragma unroll
-      for (int j = 0; j < TNU; ++j)
-#pragma unroll
-        for (int i = 0; i < TMU; ++i)
-          accq[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wq[j]), __builtin_bit_cast(h8, xu[i]),
-                                                              accq[j][i], 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < TNP; ++j)
-#pragma unroll
-        for (int i = 0; i < TMP; ++i)
-          accp[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wp[j]), __builtin_bit_cast(h8, xp[i]),
-                                                              accp[j][i], 0, 0, 0);
-    }
-  };
-
-  u4 ra[4], rp[RB], rq[RB];
-  gload(0, ra, rp, rq);
-  lstore(0, ra, rp, rq);
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    if (kt + 1 < nk) gload(kt + 1, ra, rp, rq);
-    compute(kt & 1);
-    if (kt + 1 < nk) lstore((kt & 1) ^ 1, ra, rp, rq);
-    __syncthreads();
-  }
-
-  // epilogue: one staged tile, plain rows [0, BMU) then pooled rows [BMU, BMU + BMP)
-  unsigned char* Cs = smem;
-  uint32_t* yrow = reinterpret_cast<uint32_t*>(smem + (BMU + BMP) * CPITCH);
-  if (tid < BMU + BMP) {
-    const int w = tid < BMU ? tid / BMP : 0;
-    const int m = m0 + (tid < BMU ? tid % BMP : tid - BMU);
-    uint32_t v = ~0u;
-    if (m < p.M) {
-      PixelWalk pw(p, m);
-      v = tid < BMU ? (uint32_t)(pix_index(pw.b, 2 * pw.ho + (w >> 1), 2 * pw.wo + (w & 1), q.Ho, q.Wo) * q.yc + q.yoff)
-                    : (uint32_t)(pix_index(pw.b, pw.ho, pw.wo, p.Ho, p.Wo) * p.yc + p.yoff);
-    }
-    yrow[tid] = v;
-  }
-  with_act(p.act, [&](auto actc) {
-    constexpr int ACT = decltype(actc)::value;
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-#pragma unroll
-    for (int j = 0; j < TNU; ++j)
-#pragma unroll
-      for (int i = 0; i < TMU; ++i) {
-        const int row = wave * BMP + i * 16 + li, col = j * 16 + g * 4;
-        h4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (_Float16)act_t<ACT>(accq[j][i][e]);
-        *reinterpret_cast<h4*>(Cs + row * CPITCH + col * 2) = v;
-      }
-#pragma unroll
-    for (int j = 0; j < TNP; ++j)
-#pragma unroll
-      for (int i = 0; i < TMP; ++i) {
-        const int row = BMU + i * 16 + li, col = wave * (BN / 4) + j * 16 + g * 4;
-        h4 v;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (_Float16)act_t<ACT>(accp[j][i][e]);
-        *reinterpret_cast<h4*>(Cs + row * CPITCH + col * 2) = v;
-      }
-  });
-  __syncthreads();
-  constexpr int CPR = BN * 2 / 16;
-  static_assert((BMU + BMP) * CPR % NT == 0, "whole store rounds");
-  _Float16* __restrict__ yq = reinterpret_cast<_Float16*>(q.y);
-  _Float16* __restrict__ yp = reinterpret_cast<_Float16*>(p.y);
-#pragma unroll
-  for (int k = 0; k < (BMU + BMP) * CPR / NT; ++k) {
-    const int cc = tid + k * NT;
-    const int row = cc / CPR, ch = cc - row * CPR;
-    const uint32_t yo = yrow[row];
-    const int n = n0 + ch * 8;
-    if (yo != ~0u && n < p.cout)
-      *reinterpret_cast<u4*>((row < BMU ? yq : yp) + yo + n) = *reinterpret_cast<const u4*>(Cs + row * CPITCH + ch * 16);
-  }
-}
-
 // Split-K hand-off between the S blocks of one output tile (last arriver reduces).  Every block
 // publishes its fp32 partial tile ([TN*TM][NTH] float4, coalesced) to p.part, then counts itself in
 // p.cnt[tile]; the block that counts last sums the S partials in split order 0..S-1 (the result does
@@ -2481,33 +2270,6 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   if (p.cout <= 32) return one ? launch_t<128, 32, 4, true, false>(p, st) : launch_t<128, 32, 4, false, false>(p, st);
   if (p.cout <= 64) return one ? launch_t<128, 64, 2, true, false>(p, st) : launch_t<128, 64, 2, false, false>(p, st);
   return one ? launch_t<128, 128, 2, true, false>(p, st) : launch_t<128, 128, 2, false, false>(p, st);
-}
-
-// MP twin (conv_f16_twin_kernel): the pooled 1x1 conv p and the plain 1x1 conv q of one MP block,
-// one launch.  YV7_TWIN: 1 (default) BN 64 with two blocks per CU, 2 BN 128 with one, 0 off.
-int twin_form() {
-  static const int f = [] { const char* e = getenv("YV7_TWIN"); return e ? atoi(e) : 1; }();
-  return f;
-}
-
-bool twin_supported(const ConvParams& p, const ConvParams& q) {
-  return twin_form() != 0 && p.pool == 2 && p.k == 1 && p.s == 2 && p.pad == 0 && q.pool == 0 && q.k == 1 &&
-         q.s == 1 && q.pad == 0 && p.x == q.x && p.xoff == q.xoff && p.xc == q.xc && p.cin == q.cin &&
-         p.cin % BKE == 0 && p.kpad == q.kpad && p.cout == q.cout && p.cout % 8 == 0 && p.act == q.act &&
-         p.H == q.H && p.W == q.W && q.Ho == 2 * p.Ho && q.Wo == 2 * p.Wo && q.Ho == q.H && q.Wo == q.W &&
-         p.yoff % 8 == 0 && p.yc % 8 == 0 && q.yoff % 8 == 0 && q.yc % 8 == 0 && p.variant == 0 && q.variant == 0;
-}
-
-hipError_t launch_conv_twin_f16(const ConvParams& p, const ConvParams& q, hipStream_t st) {
-  if (!twin_supported(p, q)) return hipErrorInvalidValue;
-  constexpr int BMP = 32;
-  const int nM = (p.M + BMP - 1) / BMP;
-  if (twin_form() == 2) {
-    YV7_LAUNCH((conv_f16_twin_kernel<BMP, 128, 1>), dim3(nM * ((p.cout + 127) / 128)), dim3(NT), 0, st, p, q);
-  } else {
-    YV7_LAUNCH((conv_f16_twin_kernel<BMP, 64, 2>), dim3(nM * ((p.cout + 63) / 64)), dim3(NT), 0, st, p, q);
-  }
-  return hipGetLastError();
 }
 
 }  // namespace yv7

@@ -482,45 +482,22 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
       }
       case YV7_OP_CONV:
       case YV7_OP_DETECT: {
-        if (fused_until > i) break;   // launched with the previous op (MP twin)
-        auto operands = [&](size_t op, yv7::ConvParams& c) {
-          const auto& q = p->ops[op];
-          c.x = wsb + off[q.src];
-          c.w = wb + q.w_off;
-          c.bias = reinterpret_cast<const float*>(wb + q.b_off);
-          c.zero = p->zero;
-          c.part = reinterpret_cast<float*>(wsb + scr.part_off);
-          c.part_bytes = scr.part_bytes;
-          c.cnt = reinterpret_cast<int*>(wsb + scr.cnt_off);
-          c.cnt_n = scr.cnt_n;
-          if (q.kind == YV7_OP_CONV) {
-            const auto& to = p->tensors[q.dst];
-            c.y = wsb + off[q.dst];
-            c.yc = to.channels;
-            c.yoff = q.dst_coff;
-          }
-        };
         yv7::ConvParams c = conv_params(p, i, B, H, W);
-        operands(i, c);
+        c.x = wsb + off[o.src];
+        c.w = wb + o.w_off;
+        c.bias = reinterpret_cast<const float*>(wb + o.b_off);
+        c.zero = p->zero;
+        c.part = reinterpret_cast<float*>(wsb + scr.part_off);
+        c.part_bytes = scr.part_bytes;
+        c.cnt = reinterpret_cast<int*>(wsb + scr.cnt_off);
+        c.cnt_n = scr.cnt_n;
         if (o.kind == YV7_OP_CONV) {
           const auto& to = p->tensors[o.dst];
           if (c.Ho != (H >> to.shift) || c.Wo != (W >> to.shift))
             return fail(YV7_E_SHAPE, "yv7_forward: op " + std::to_string(i) + " output shape mismatch");
-          // yolov7's MP block: this MP-folded 1x1 conv and the next op's 1x1 conv read one tensor —
-          // one launch for both (conv_f16.hip conv_f16_twin_kernel); the next op records no time
-          if (p->dtype == YV7_DT_F16 && o.pool == 2 && !is_f8(o) && i + 1 < p->ops.size()) {
-            const auto& o2 = p->ops[i + 1];
-            if (o2.kind == YV7_OP_CONV && !is_f8(o2) && o2.src == o.src && o2.src_coff == o.src_coff) {
-              yv7::ConvParams c2 = conv_params(p, i + 1, B, H, W);
-              operands(i + 1, c2);
-              const auto& t2 = p->tensors[o2.dst];
-              if (c2.Ho == (H >> t2.shift) && c2.Wo == (W >> t2.shift) && yv7::twin_supported(c, c2)) {
-                e = yv7::launch_conv_twin_f16(c, c2, st);
-                fused_until = i + 2;
-                break;
-              }
-            }
-          }
+          c.y = wsb + off[o.dst];
+          c.yc = to.channels;
+          c.yoff = o.dst_coff;
           if (is_f8(o)) {
             // 82: the fp8 GEMM quantizes the fp16 input slice on its way into LDS (no staging pass, but
             // every N tile of a row block converts it again: VALU work ~2x the block's MFMA time per

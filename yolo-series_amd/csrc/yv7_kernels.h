@@ -164,10 +164,6 @@ struct StemParams {
 hipError_t launch_conv(int dtype, const ConvParams& p, bool detect, hipStream_t st);
 bool det_writes_rowbest(int dtype);   // true when the head kernel launch_conv picks fills ConvParams::best
 hipError_t launch_conv_f16(const ConvParams& p, bool detect, hipStream_t st);
-// yolov7's MP block as one launch: p = the 1x1 conv over the 2x2 max (pool = 2), q = the 1x1 conv of
-// the same input slice (conv_f16.hip, conv_f16_twin_kernel)
-bool twin_supported(const ConvParams& p, const ConvParams& q);
-hipError_t launch_conv_twin_f16(const ConvParams& p, const ConvParams& q, hipStream_t st);
 bool halo_supported(const ConvParams& p);
 bool ws64_supported(const ConvParams& p);
 hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st);
