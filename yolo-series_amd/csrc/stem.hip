@@ -327,23 +327,35 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
     for (int e = 0; e < 4; ++e) bb_l[j][e] = p.bb[(2 * ng + j) * 16 + g * 4 + e] * sb_scale;
 
   constexpr int PPT = (PY * PX + NT - 1) / NT;
-  S pre[PPT][3];
+  // raw loaded bits (fp16 input: 16-bit, fp32: 32-bit), left untouched until the commit: converting,
+  // zero-extending or packing two halves into one register right after the loads makes the wave wait
+  // on them there instead of a tile later
+  typedef std::conditional_t<sizeof(S) == 2, unsigned short, uint32_t> Bits;
+  Bits pre[PPT][3];
+  // image loads as unconditional buffer loads (a pixel outside the image reads an offset past the
+  // buffer: zero), so no branch hides them from the compiler's wait counting — a branchy load lets
+  // it fall back to vmcnt(0), which also waits for the previous tile's output stores
+  const uint32_t plane = (uint32_t)(p.H * p.W * sizeof(S));
+  const auto xr = make_rsrc(p.x, (uint32_t)((size_t)p.B * 3 * plane));
   auto prefetch = [&](int t) {
     int tb, ty, tx;
     tile_geom(t, tb, ty, tx);
     const int iy0 = SA * (2 * ty - 1) - 1, ix0 = SA * (2 * tx - 1) - 1;
-    const S* xb = reinterpret_cast<const S*>(p.x) + (size_t)tb * 3 * p.H * p.W;
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
       const int i = tid + k * NT;
       const int py = i / PX, px = i - py * PX;
       const int iy = iy0 + py, ix = ix0 + px;
-      pre[k][0] = pre[k][1] = pre[k][2] = (S)0.f;
-      if (i < PY * PX && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2) {
-        const size_t o = (size_t)iy * p.W + ix;
-        pre[k][0] = xb[o];
-        pre[k][1] = xb[o + (size_t)p.H * p.W];
-        pre[k][2] = xb[o + 2 * (size_t)p.H * p.W];
+      const bool in = i < PY * PX && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2;
+      // 24-bit multiply (a v_mad_u64_u32 here took a pending load's register as its don't-care high
+      // half, stalling the prefetch on its own loads)
+      const uint32_t o = in ? (uint32_t)tb * 3u * plane + (__umul24(iy, p.W) + ix) * (uint32_t)sizeof(S) : 0x80000000u;
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) {
+        if constexpr (sizeof(S) == 2)
+          pre[k][ch] = __builtin_amdgcn_raw_buffer_load_b16(xr, o + ch * plane, 0, 0);
+        else
+          pre[k][ch] = __builtin_amdgcn_raw_buffer_load_b32(xr, o + ch * plane, 0, 0);
       }
     }
   };
@@ -352,8 +364,15 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
     for (int k = 0; k < PPT; ++k) {
       const int i = tid + k * NT;
       typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      const h4 v = {(_Float16)(float)pre[k][0], (_Float16)(float)pre[k][1], (_Float16)(float)pre[k][2],
-                    (_Float16)0.f};
+      // the loads are consumed here and not earlier: the compiler would otherwise pack two halves
+      // into one register right after the loads, waiting for them there
+#pragma unroll
+      for (int ch = 0; ch < 3; ++ch) asm volatile("" : "+v"(pre[k][ch]));
+      auto val = [&](Bits bits) -> _Float16 {
+        if constexpr (sizeof(S) == 2) return __builtin_bit_cast(_Float16, bits);
+        else return (_Float16)__builtin_bit_cast(float, bits);
+      };
+      const h4 v = {val(pre[k][0]), val(pre[k][1]), val(pre[k][2]), (_Float16)0.f};
       if (i < PY * PX) *reinterpret_cast<h4*>(patch + i * 4) = v;
     }
   };
@@ -401,19 +420,20 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
   const int vb = G % 8 == 0 ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
   if (vb < ntiles) prefetch(vb);
   int pb = -1, poy0 = 0, pox0 = 0;   // the previous tile (its staged output is stored in this iteration)
+  // output stores likewise unconditional (a pixel past the image edge stores past the buffer: dropped)
+  const auto yr = make_rsrc(p.y, (uint32_t)(bordered_pixels(p.B, HB, WB) * p.yc * 2));
   auto store_prev = [&]() {
     if (pb < 0) return;
     constexpr int CPR = CB * 2 / 16;
-    _Float16* y = reinterpret_cast<_Float16*>(p.y);
 #pragma unroll
     for (int k = 0; k < TBY * TBX * CPR / NT; ++k) {
       const int c = tid + k * NT;
       const int mb = c / CPR, ch = c - mb * CPR;
       const int ty = mb / TBX, tx = mb - ty * TBX;
       const int oy = poy0 + ty, ox = pox0 + tx;
-      if (oy < HB && ox < WB && p.variant != 4)
-        *reinterpret_cast<u4*>(y + pix_index(pb, oy, ox, HB, WB) * p.yc + p.yoff + ch * 8) =
-            *reinterpret_cast<const u4*>(obuf + mb * CPITCH + ch * 16);
+      const bool in = oy < HB && ox < WB && p.variant != 4;
+      const uint32_t o = in ? (uint32_t)((pix_index(pb, oy, ox, HB, WB) * p.yc + p.yoff + ch * 8) * 2) : 0x80000000u;
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u4*>(obuf + mb * CPITCH + ch * 16), yr, o, 0, 0);
     }
   };
   for (int tile = vb; tile < ntiles; tile += G) {
