@@ -326,15 +326,17 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) bb_l[j][e] = p.bb[(2 * ng + j) * 16 + g * 4 + e] * sb_scale;
 
-  constexpr int PPT = (PY * PX + NT - 1) / NT;
-  // raw loaded bits (fp16 input: 16-bit, fp32: 32-bit), left untouched until the commit: converting,
-  // zero-extending or packing two halves into one register right after the loads makes the wave wait
-  // on them there instead of a tile later
-  typedef std::conditional_t<sizeof(S) == 2, unsigned short, uint32_t> Bits;
-  Bits pre[PPT][3];
-  // image loads as unconditional buffer loads (a pixel outside the image reads an offset past the
-  // buffer: zero), so no branch hides them from the compiler's wait counting — a branchy load lets
-  // it fall back to vmcnt(0), which also waits for the previous tile's output stores
+  // The image patch: fp16 input (the bench path) moves horizontally adjacent pixel PAIRS — one dword
+  // per channel plane (the patch's x origin 2 tx - 2 is even and so is W, so a pair lies wholly inside
+  // or wholly outside the image), a third of the load instructions of one pixel per lane; fp32 input
+  // one pixel per lane.  Raw loaded bits stay untouched until the commit: converting or packing them
+  // right after the loads makes the wave wait on them there instead of a tile later.
+  constexpr bool PAIRS = sizeof(S) == 2;
+  constexpr int UPR = PAIRS ? (PX + 1) / 2 : PX;        // load units per patch row
+  constexpr int PPT = (PY * UPR + NT - 1) / NT;
+  uint32_t pre[PPT][3];
+  // unconditional buffer loads (outside the image: an offset past the buffer reads zero), so no branch
+  // hides them from the compiler's wait counting
   const uint32_t plane = (uint32_t)(p.H * p.W * sizeof(S));
   const auto xr = make_rsrc(p.x, (uint32_t)((size_t)p.B * 3 * plane));
   auto prefetch = [&](int t) {
@@ -344,36 +346,37 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
       const int i = tid + k * NT;
-      const int py = i / PX, px = i - py * PX;
-      const int iy = iy0 + py, ix = ix0 + px;
-      const bool in = i < PY * PX && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2;
+      const int py = i / UPR, ux = i - py * UPR;
+      const int iy = iy0 + py, ix = ix0 + (PAIRS ? 2 * ux : ux);
+      const bool in = i < PY * UPR && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2;
       // 24-bit multiply (a v_mad_u64_u32 here took a pending load's register as its don't-care high
       // half, stalling the prefetch on its own loads)
       const uint32_t o = in ? (uint32_t)tb * 3u * plane + (__umul24(iy, p.W) + ix) * (uint32_t)sizeof(S) : 0x80000000u;
 #pragma unroll
-      for (int ch = 0; ch < 3; ++ch) {
-        if constexpr (sizeof(S) == 2)
-          pre[k][ch] = __builtin_amdgcn_raw_buffer_load_b16(xr, o + ch * plane, 0, 0);
-        else
-          pre[k][ch] = __builtin_amdgcn_raw_buffer_load_b32(xr, o + ch * plane, 0, 0);
-      }
+      for (int ch = 0; ch < 3; ++ch) pre[k][ch] = __builtin_amdgcn_raw_buffer_load_b32(xr, o + ch * plane, 0, 0);
     }
   };
   auto commit = [&]() {
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
       const int i = tid + k * NT;
-      typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-      // the loads are consumed here and not earlier: the compiler would otherwise pack two halves
-      // into one register right after the loads, waiting for them there
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) asm volatile("" : "+v"(pre[k][ch]));
-      auto val = [&](Bits bits) -> _Float16 {
-        if constexpr (sizeof(S) == 2) return __builtin_bit_cast(_Float16, bits);
-        else return (_Float16)__builtin_bit_cast(float, bits);
-      };
-      const h4 v = {val(pre[k][0]), val(pre[k][1]), val(pre[k][2]), (_Float16)0.f};
-      if (i < PY * PX) *reinterpret_cast<h4*>(patch + i * 4) = v;
+      if constexpr (PAIRS) {
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        const h2 c0 = __builtin_bit_cast(h2, pre[k][0]), c1 = __builtin_bit_cast(h2, pre[k][1]),
+                 c2 = __builtin_bit_cast(h2, pre[k][2]);
+        const int py = i / UPR, px = 2 * (i - py * UPR);
+        if (i < PY * UPR) {
+          *reinterpret_cast<h4*>(patch + (py * PX + px) * 4) = h4{c0[0], c1[0], c2[0], (_Float16)0.f};
+          if (px + 1 < PX) *reinterpret_cast<h4*>(patch + (py * PX + px + 1) * 4) = h4{c0[1], c1[1], c2[1], (_Float16)0.f};
+        }
+      } else {
+        const h4 v = {(_Float16)__builtin_bit_cast(float, pre[k][0]), (_Float16)__builtin_bit_cast(float, pre[k][1]),
+                      (_Float16)__builtin_bit_cast(float, pre[k][2]), (_Float16)0.f};
+        if (i < PY * PX) *reinterpret_cast<h4*>(patch + i * 4) = v;
+      }
     }
   };
   // conv A's K layout (as stem_kernel): two taps per 8-half lane group
