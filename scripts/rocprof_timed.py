@@ -24,7 +24,7 @@ fwd = -1
 per = {}
 for r in rows:
     n = r['Kernel_Name']
-    if 'stem_kernel' in n:
+    if 'stem_kernel' in n or 'stem2_kernel' in n:
         fwd += 1
     dur = (int(r['End_Timestamp']) - int(r['Start_Timestamp'])) / 1e3
     fam = 'conv' if any(c in n for c in CONV) else ('nms' if any(c in n for c in NMS) else None)
