@@ -1953,13 +1953,6 @@ hipError_t launch_p8w(const ConvParams& p, bool one, hipStream_t st) {
   return hipGetLastError();
 }
 
-// YV7_PRING3=1: the 128 x 128 persistent ring as three blocks per CU (variant 218) where the dispatch
-// runs it with two (A/B switch)
-bool pring3() {
-  static const int on = [] { const char* e = getenv("YV7_PRING3"); return e ? atoi(e) : 0; }();
-  return on != 0;
-}
-
 // 128-channel 3x3 stride-1 layers with at least one round of 512 x 128 tiles on the 8-phase ring
 // (variant 238) — YV7_P8W=1 (bench A/B under batches in flight: alone on the chip it ties the 2-phase
 // ring, the last partial round of its 400 tiles leaving CUs idle that other streams can fill).
@@ -2178,7 +2171,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
       if (p.K >= 256 && p.cout >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
       if (wide && p.cout >= 256 && t256 >= 200) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
       if (p.K <= 512 && p.M >= 51200)
-        return pring3() ? launch_pring<128, 128, 2, 2, 3, 32>(p, one, 3, st) : launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
+        return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     } else if (wide && p.k == 3 && p.cin >= 256 && p.cout >= 256 && t256 >= 200) {
       return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
     } else if (p8w_default(p)) {
@@ -2187,7 +2180,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
       // (3x3 512->512 @20 and s2 from @40 take the non-persistent 128 x 128 ring of choose() below:
       // in-network 92 (this ring) / 89 (256 x 128 persistent) -> 79 us; with fewer tiles than CUs,
       // yolov7-w6 at bs 8, it splits K: 72 -> 35 us)
-      return pring3() ? launch_pring<128, 128, 2, 2, 3, 32>(p, one, 3, st) : launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
+      return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     }
   }
   const Choice ch = choose(p, det);
@@ -2209,8 +2202,9 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 215) return launch_pring<256, 128, 2, 2, 3, 32>(p, one, 2, st);
     if (variant == 216) return launch_pring<128, 256, 2, 2, 3, 32>(p, one, 2, st);
     if (variant == 217) return launch_pring<128, 128, 2, 2, 2, 64>(p, one, 2, st);
-    // three blocks per CU (48 KiB of ring each): more waves to hide the ring's latency, and room for a
-    // block of another stream's kernel beside two of these
+    // three blocks per CU (48 KiB of ring each): more waves to hide the ring's latency — measured
+    // 10-20 % slower than the dispatch on every 128-channel layer, bench 6626 vs 6801 img/s
+    // (profiles/r2c_pring3/): twice the barriers per K of 64 cost more than the extra waves hide
     if (variant == 218) return launch_pring<128, 128, 2, 2, 3, 32>(p, one, 3, st);
     // pipelined persistent rings (conv_f16_pp_kernel)
     if (variant == 221) return one ? launch_pp<256, 256, 2, 4, true>(p, 1, st) : launch_pp<256, 256, 2, 4, false>(p, 1, st);
