@@ -284,7 +284,7 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
   constexpr int MA = (NA + 15) / 16;
   constexpr int APITCH = CA * 2 + 16;
   constexpr int PATCH = (PY * PX * 8 + 15) / 16 * 16;
-  constexpr int ABUF = (NA * APITCH + 15) / 16 * 16;
+  constexpr int ABUF = MA * 16 * APITCH;            // whole m-tiles: conv A's writes need no row guard
   constexpr int MB = TBY * TBX / 16;
   constexpr int CPITCH = CB * 2 + 16;
   constexpr int OUTB = TBY * TBX * CPITCH;
@@ -369,12 +369,12 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
                  c2 = __builtin_bit_cast(h2, pre[k][2]);
         const int py = i / UPR, px = 2 * (i - py * UPR);
         if (i < PY * UPR) {
-          *reinterpret_cast<h4*>(patch + (py * PX + px) * 4) = h4{c0[0], c1[0], c2[0], (_Float16)0.f};
-          if (px + 1 < PX) *reinterpret_cast<h4*>(patch + (py * PX + px + 1) * 4) = h4{c0[1], c1[1], c2[1], (_Float16)0.f};
+          *reinterpret_cast<h4*>(patch + (py * PX + px) * 4) = h4{c0[0], c1[0], c2[0], (_Float16)1.f};
+          if (px + 1 < PX) *reinterpret_cast<h4*>(patch + (py * PX + px + 1) * 4) = h4{c0[1], c1[1], c2[1], (_Float16)1.f};
         }
       } else {
         const h4 v = {(_Float16)__builtin_bit_cast(float, pre[k][0]), (_Float16)__builtin_bit_cast(float, pre[k][1]),
-                      (_Float16)__builtin_bit_cast(float, pre[k][2]), (_Float16)0.f};
+                      (_Float16)__builtin_bit_cast(float, pre[k][2]), (_Float16)1.f};
         if (i < PY * PX) *reinterpret_cast<h4*>(patch + i * 4) = v;
       }
     }
@@ -387,6 +387,10 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
     }
     return (gg == 0 && half == 0) ? 8 : -1;
   };
+  // conv A's bias rides in the MFMA: every patch pixel's 4th channel is 1.0, and the weight slots of
+  // that channel carry the bias as two fp16 parts (tap (0,0): hi, tap (0,1): the remainder, exact to
+  // ~2^-22 of it) — the accumulators start at the inline constant 0, no bias copies per tile.  Slots
+  // with no tap (K step 1 but for tap (2,2)) read patch pixel 0 against zero weights.
   constexpr int NAT = CA / 16;
   u4 wa[2][NAT];
 #pragma unroll
@@ -396,12 +400,15 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
       typedef _Float16 h8v __attribute__((ext_vector_type(8)));
       h8v w8;
       const _Float16* wrow = reinterpret_cast<const _Float16*>(p.wa) + (size_t)(nt * 16 + li) * p.kpad_a;
+      const float bs = p.ba[nt * 16 + li] * sa_scale;
+      const _Float16 bhi = (_Float16)bs, blo = (_Float16)(bs - (float)bhi);
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int tap = tap_of(ks, g, h2);
 #pragma unroll
-        for (int ci = 0; ci < 4; ++ci)
-          w8[h2 * 4 + ci] = (tap >= 0 && ci < 3) ? (_Float16)((float)wrow[tap * 3 + ci] * sa_scale) : (_Float16)0.f;
+        for (int ci = 0; ci < 3; ++ci)
+          w8[h2 * 4 + ci] = tap >= 0 ? (_Float16)((float)wrow[tap * 3 + ci] * sa_scale) : (_Float16)0.f;
+        w8[h2 * 4 + 3] = tap == 0 ? bhi : tap == 1 ? blo : (_Float16)0.f;
       }
       wa[ks][nt] = __builtin_bit_cast(u4, w8);
     }
@@ -411,13 +418,8 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
 #pragma unroll
     for (int h2 = 0; h2 < 2; ++h2) {
       const int tap = tap_of(ks, g, h2);
-      toff[ks][h2] = tap >= 0 ? ((tap / 3) * PX + tap % 3) * 8 : -1;
+      toff[ks][h2] = tap >= 0 ? ((tap / 3) * PX + tap % 3) * 8 : 0;
     }
-  float ba_l[NAT][4];
-#pragma unroll
-  for (int nt = 0; nt < NAT; ++nt)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) ba_l[nt][e] = p.ba[nt * 16 + g * 4 + e] * sa_scale;
 
   const int G = gridDim.x;
   const int vb = G % 8 == 0 ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
@@ -456,7 +458,7 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
       for (int grp = 0; grp < MA / 12; ++grp) {
         u4 xv[3][2];
         int mm[3];
-        bool inside[3];
+        uint32_t keep[3];
 #pragma unroll
         for (int u = 0; u < 3; ++u) {
           const int m = (grp * 3 + u) * 4 * 16 + wave * 16 + li;   // m-tile (grp*3+u)*4 + wave
@@ -466,22 +468,20 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
           const int base = (SA * yl * PX + SA * xl) * 8;
 #pragma unroll
           for (int ks = 0; ks < 2; ++ks) {
-            u2 lo = {0u, 0u}, hi = {0u, 0u};
-            if (toff[ks][0] >= 0) lo = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][0]);
-            if (toff[ks][1] >= 0) hi = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][1]);
+            const u2 lo = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][0]);
+            const u2 hi = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][1]);
             xv[u][ks] = u4{lo[0], lo[1], hi[0], hi[1]};
           }
           const int ay = ay0 + yl, ax = ax0 + xl;
-          inside[u] = m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA;
+          keep[u] = (m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA) ? ~0u : 0u;
         }
         f4 acc[3][NAT];
 #pragma unroll
         for (int u = 0; u < 3; ++u)
 #pragma unroll
           for (int nt = 0; nt < NAT; ++nt) {
-            f4 a = {ba_l[nt][0], ba_l[nt][1], ba_l[nt][2], ba_l[nt][3]};
-            a = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[0][nt]), __builtin_bit_cast(h8, xv[u][0]),
-                                                       a, 0, 0, 0);
+            const f4 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[0][nt]),
+                                                                 __builtin_bit_cast(h8, xv[u][0]), f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
             acc[u][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[1][nt]),
                                                                 __builtin_bit_cast(h8, xv[u][1]), a, 0, 0, 0);
           }
@@ -489,17 +489,17 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
         for (int u = 0; u < 3; ++u)
 #pragma unroll
           for (int nt = 0; nt < NAT; ++nt) {
-            typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-            h4 o;
+            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+            float v[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-              float v;
-              if (p.variant == 1) v = acc[u][nt][e];
-              else if constexpr (ACT_A == 1) v = acc[u][nt][e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[u][nt][e]));
-              else v = act_t<ACT_A>(acc[u][nt][e]);
-              o[e] = inside[u] ? (_Float16)v : (_Float16)0.f;
+              if constexpr (ACT_A == 1) v[e] = acc[u][nt][e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[u][nt][e]));
+              else v[e] = act_t<ACT_A>(acc[u][nt][e]);
             }
-            if (mm[u] < NA) *reinterpret_cast<h4*>(abuf + mm[u] * APITCH + (nt * 16 + g * 4) * 2) = o;
+            // zero outside the image (conv B's padding): one mask per packed pair of halves
+            const u2 o = {__builtin_bit_cast(uint32_t, h2{(_Float16)v[0], (_Float16)v[1]}) & keep[u],
+                          __builtin_bit_cast(uint32_t, h2{(_Float16)v[2], (_Float16)v[3]}) & keep[u]};
+            *reinterpret_cast<u2*>(abuf + mm[u] * APITCH + (nt * 16 + g * 4) * 2) = o;
           }
       }
     }
