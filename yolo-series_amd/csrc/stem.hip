@@ -339,19 +339,26 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
   // hides them from the compiler's wait counting
   const uint32_t plane = (uint32_t)(p.H * p.W * sizeof(S));
   const auto xr = make_rsrc(p.x, (uint32_t)((size_t)p.B * 3 * plane));
+  // per-thread unit geometry, fixed across tiles
+  int u_py[PPT], u_px[PPT];
+#pragma unroll
+  for (int k = 0; k < PPT; ++k) {
+    const int i = tid + k * NT;
+    u_py[k] = i < PY * UPR ? i / UPR : -0x40000;   // units past the patch: a row that is never inside
+    u_px[k] = (PAIRS ? 2 : 1) * (i - (i / UPR) * UPR);
+  }
   auto prefetch = [&](int t) {
     int tb, ty, tx;
     tile_geom(t, tb, ty, tx);
     const int iy0 = SA * (2 * ty - 1) - 1, ix0 = SA * (2 * tx - 1) - 1;
+    const uint32_t img = (uint32_t)tb * 3u * plane;
 #pragma unroll
     for (int k = 0; k < PPT; ++k) {
-      const int i = tid + k * NT;
-      const int py = i / UPR, ux = i - py * UPR;
-      const int iy = iy0 + py, ix = ix0 + (PAIRS ? 2 * ux : ux);
-      const bool in = i < PY * UPR && (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2;
+      const int iy = iy0 + u_py[k], ix = ix0 + u_px[k];
+      const bool in = (unsigned)iy < (unsigned)p.H && (unsigned)ix < (unsigned)p.W && p.variant != 2;
       // 24-bit multiply (a v_mad_u64_u32 here took a pending load's register as its don't-care high
       // half, stalling the prefetch on its own loads)
-      const uint32_t o = in ? (uint32_t)tb * 3u * plane + (__umul24(iy, p.W) + ix) * (uint32_t)sizeof(S) : 0x80000000u;
+      const uint32_t o = in ? img + (__umul24(iy, p.W) + ix) * (uint32_t)sizeof(S) : 0x80000000u;
 #pragma unroll
       for (int ch = 0; ch < 3; ++ch) pre[k][ch] = __builtin_amdgcn_raw_buffer_load_b32(xr, o + ch * plane, 0, 0);
     }
@@ -427,18 +434,28 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
   int pb = -1, poy0 = 0, pox0 = 0;   // the previous tile (its staged output is stored in this iteration)
   // output stores likewise unconditional (a pixel past the image edge stores past the buffer: dropped)
   const auto yr = make_rsrc(p.y, (uint32_t)(bordered_pixels(p.B, HB, WB) * p.yc * 2));
+  // per-thread store geometry: staging chunk -> (pixel row, column, channel byte offset)
+  constexpr int CPR = CB * 2 / 16;
+  constexpr int NSTO = TBY * TBX * CPR / NT;
+  int s_ty[NSTO], s_tx[NSTO], s_mbo[NSTO];
+  uint32_t s_rel[NSTO];
+#pragma unroll
+  for (int k = 0; k < NSTO; ++k) {
+    const int c = tid + k * NT;
+    const int mb = c / CPR, ch = c - mb * CPR;
+    s_ty[k] = mb / TBX;
+    s_tx[k] = mb - s_ty[k] * TBX;
+    s_mbo[k] = mb * CPITCH + ch * 16;
+    s_rel[k] = (uint32_t)(((s_ty[k] * (WB + 2 * BORDER) + s_tx[k]) * p.yc + p.yoff + ch * 8) * 2);
+  }
   auto store_prev = [&]() {
     if (pb < 0) return;
-    constexpr int CPR = CB * 2 / 16;
+    const uint32_t tile_off = (uint32_t)(pix_index(pb, poy0, pox0, HB, WB) * p.yc * 2);
 #pragma unroll
-    for (int k = 0; k < TBY * TBX * CPR / NT; ++k) {
-      const int c = tid + k * NT;
-      const int mb = c / CPR, ch = c - mb * CPR;
-      const int ty = mb / TBX, tx = mb - ty * TBX;
-      const int oy = poy0 + ty, ox = pox0 + tx;
-      const bool in = oy < HB && ox < WB && p.variant != 4;
-      const uint32_t o = in ? (uint32_t)((pix_index(pb, oy, ox, HB, WB) * p.yc + p.yoff + ch * 8) * 2) : 0x80000000u;
-      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u4*>(obuf + mb * CPITCH + ch * 16), yr, o, 0, 0);
+    for (int k = 0; k < NSTO; ++k) {
+      const bool in = poy0 + s_ty[k] < HB && pox0 + s_tx[k] < WB && p.variant != 4;
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u4*>(obuf + s_mbo[k]), yr,
+                                             in ? tile_off + s_rel[k] : 0x80000000u, 0, 0);
     }
   };
   for (int tile = vb; tile < ntiles; tile += G) {
