@@ -903,7 +903,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
   AWalk<ONE, RA, BK> aw;
   uint32_t b_off[RB];
   int ig = 0, it = 0, ikt = 0;
-  auto issue_next = [&]() {
+  auto issue_next = [&]() __attribute__((always_inline)) {
     if (ikt == 0) {
       const int t = tw.at(it);
       const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
@@ -934,7 +934,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
   // ---- compute cursor
   f4 acc[TN][TM];
   int cm0 = 0, cn0 = 0;
-  auto init_tile = [&](int i) {
+  auto init_tile = [&](int i) __attribute__((always_inline)) {
     const int t = tw.at(i);
     cm0 = (t / nN) * BM;
     cn0 = (t % nN) * BN;
@@ -949,7 +949,14 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
     }
   };
   const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
-  auto epilogue = [&]() {
+  auto epilogue = [&]() __attribute__((always_inline)) {
+    // the accumulators are final only here: without this the compiler speculates the activation's
+    // first instructions (scale, v_exp) for every accumulator into every K step, ahead of the
+    // tile-end branch (~20 VALU per step on the 128 x 128 ring)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int ii = 0; ii < TM; ++ii) asm volatile("" : "+v"(acc[j][ii]));
     if (p.variant == 296 || p.variant == 297) {   // microbenchmark hooks: 296 activation, no stores; 297 neither
       float sink = 0.0f;
 #pragma unroll
@@ -997,7 +1004,11 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
   init_tile(0);
 
   int ci = 0, ckt = 0;
-  for (int gs = 0; gs < nsteps; ++gs) {
+  // One K step; SLOT = gs % STAGES as a compile-time constant (the loop below is unrolled by STAGES),
+  // so every fragment read is a loop-invariant per-lane offset plus an immediate slot offset — no
+  // address arithmetic per read and step.
+  auto kstep = [&](int gs, auto slotc) __attribute__((always_inline)) {
+    constexpr int SLOT = decltype(slotc)::value;   // -1: gs % STAGES at run time
     // stage gs has landed once at most `younger` vector-memory ops of this wave are outstanding
     const int ndma = min(STAGES - 2, nsteps - 1 - gs);
     const bool st = ci > 0 && ckt <= STAGES - 2;
@@ -1011,7 +1022,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     if (ig < nsteps) issue_next();   // refills the slot every wave finished reading at step gs-1
-    const unsigned char* As = smem + (gs % STAGES) * STAGE;
+    const unsigned char* As = smem + (SLOT >= 0 ? SLOT : gs % STAGES) * STAGE;
     const unsigned char* Bs = WS ? wl + ckt * BN * RB_ : As + BM * RB_;
     // every fragment of the step is read up front: the second sub-step's reads are in flight under
     // the first sub-step's MFMAs
@@ -1046,6 +1057,24 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
       ckt = 0;
       if (++ci < ntl) init_tile(ci);
     }
+  };
+  int gs = 0;
+  // unrolled only where every slot offset fits a ds_read immediate (16 bits): the 64 KiB stages of the
+  // 256 x 256 ring would need a second base register per slot and spill
+  constexpr bool UNROLL = STAGES * STAGE <= 65536;
+  if constexpr (!UNROLL) {
+    for (; gs < nsteps; ++gs) kstep(gs, std::integral_constant<int, -1>{});
+  }
+  for (; UNROLL && gs + STAGES <= nsteps; gs += STAGES) {
+    kstep(gs, std::integral_constant<int, 0>{});
+    kstep(gs + 1, std::integral_constant<int, 1>{});
+    if constexpr (STAGES > 2) kstep(gs + 2, std::integral_constant<int, (STAGES > 2 ? 2 : 0)>{});
+    if constexpr (STAGES > 3) kstep(gs + 3, std::integral_constant<int, (STAGES > 3 ? 3 : 0)>{});
+  }
+  if constexpr (UNROLL) {
+    if (gs < nsteps) kstep(gs++, std::integral_constant<int, 0>{});   // remainder: slots 0, 1, 2 in order
+    if (STAGES > 2 && gs < nsteps) kstep(gs++, std::integral_constant<int, 1>{});
+    if (STAGES > 3 && gs < nsteps) kstep(gs++, std::integral_constant<int, (STAGES > 3 ? 2 : 0)>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
