@@ -276,8 +276,8 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
 //   * the output staging tile has its own LDS (patch + A tile + staging = 68.6 KB, two blocks per CU),
 //     so a tile needs 3 barriers: [stores of t-1, patch of t] | conv A | conv B + staging;
 //   * both biases in registers from kernel entry (no global load inside the tile loop).
-template <typename S, int CA, int CB, int SA, int TBY, int TBX, int ACT_A, int ACT_B>
-__global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
+template <typename S, int CA, int CB, int SA, int TBY, int TBX, int ACT_A, int ACT_B, bool PIPE>
+__global__ __launch_bounds__(NT, PIPE ? 1 : 2) void stem2_kernel(const StemParams p) {
   constexpr int TAY = 2 * TBY + 1, TAX = 2 * TBX + 1;
   constexpr int PY = SA * (TAY - 1) + 3, PX = SA * (TAX - 1) + 3;
   constexpr int NA = TAY * TAX;
@@ -290,10 +290,11 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
   constexpr int OUTB = TBY * TBX * CPITCH;
   static_assert(CB == 64 && CA == 32, "4 waves = 2 m-groups x 2 n-groups of 32 channels; one MFMA k-step per tap");
   static_assert(MB == 8 && MA % 12 == 0, "conv B: 4 m-tiles per wave; conv A: groups of 3 m-tiles per wave");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[PATCH + ABUF + OUTB];
+  constexpr int NAB = PIPE ? 2 : 1;                  // A tiles in LDS (PIPE: double-buffered)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[PATCH + NAB * ABUF + OUTB];
   _Float16* patch = reinterpret_cast<_Float16*>(smem);
-  unsigned char* abuf = smem + PATCH;
-  unsigned char* obuf = smem + PATCH + ABUF;
+  unsigned char* abuf0 = smem + PATCH;
+  unsigned char* obuf = smem + PATCH + NAB * ABUF;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -458,96 +459,86 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
                                              in ? tile_off + s_rel[k] : 0x80000000u, 0, 0);
     }
   };
-  for (int tile = vb; tile < ntiles; tile += G) {
-    int b, oy0, ox0;
-    tile_geom(tile, b, oy0, ox0);
-    const int ay0 = 2 * oy0 - 1, ax0 = 2 * ox0 - 1;
-    commit();
-    if (tile + G < ntiles) prefetch(tile + G);
-    store_prev();
-    __syncthreads();   // patch of this tile in LDS; staging of the previous one read
-
-    // conv A -> abuf, three m-tiles per group
-    {
-      const unsigned char* pbytes = reinterpret_cast<const unsigned char*>(patch);
-      typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-#pragma unroll 1
-      for (int grp = 0; grp < MA / 12; ++grp) {
-        u4 xv[3][2];
-        int mm[3];
-        uint32_t keep[3];
+  // conv A of one group of three m-tiles (of 36) -> the A tile at ab
+  const unsigned char* pbytes = reinterpret_cast<const unsigned char*>(patch);
+  typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+  auto conv_a_group = [&](int grp, unsigned char* ab, int ay0, int ax0) __attribute__((always_inline)) {
+    u4 xv[3][2];
+    int mm[3];
+    uint32_t keep[3];
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-          const int m = (grp * 3 + u) * 4 * 16 + wave * 16 + li;   // m-tile (grp*3+u)*4 + wave
-          mm[u] = m;
-          const int mc = m < NA ? m : NA - 1;
-          const int yl = mc / TAX, xl = mc - yl * TAX;
-          const int base = (SA * yl * PX + SA * xl) * 8;
+    for (int u = 0; u < 3; ++u) {
+      const int m = (grp * 3 + u) * 4 * 16 + wave * 16 + li;   // m-tile (grp*3+u)*4 + wave
+      mm[u] = m;
+      const int mc = m < NA ? m : NA - 1;
+      const int yl = mc / TAX, xl = mc - yl * TAX;
+      const int base = (SA * yl * PX + SA * xl) * 8;
 #pragma unroll
-          for (int ks = 0; ks < 2; ++ks) {
-            const u2 lo = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][0]);
-            const u2 hi = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][1]);
-            xv[u][ks] = u4{lo[0], lo[1], hi[0], hi[1]};
-          }
-          const int ay = ay0 + yl, ax = ax0 + xl;
-          keep[u] = (m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA) ? ~0u : 0u;
-        }
-        f4 acc[3][NAT];
-#pragma unroll
-        for (int u = 0; u < 3; ++u)
-#pragma unroll
-          for (int nt = 0; nt < NAT; ++nt) {
-            const f4 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[0][nt]),
-                                                                 __builtin_bit_cast(h8, xv[u][0]), f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
-            acc[u][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[1][nt]),
-                                                                __builtin_bit_cast(h8, xv[u][1]), a, 0, 0, 0);
-          }
-#pragma unroll
-        for (int u = 0; u < 3; ++u)
-#pragma unroll
-          for (int nt = 0; nt < NAT; ++nt) {
-            typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-            float v[4];
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if constexpr (ACT_A == 1) v[e] = acc[u][nt][e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[u][nt][e]));
-              else v[e] = act_t<ACT_A>(acc[u][nt][e]);
-            }
-            // zero outside the image (conv B's padding): one mask per packed pair of halves
-            const u2 o = {__builtin_bit_cast(uint32_t, h2{(_Float16)v[0], (_Float16)v[1]}) & keep[u],
-                          __builtin_bit_cast(uint32_t, h2{(_Float16)v[2], (_Float16)v[3]}) & keep[u]};
-            *reinterpret_cast<u2*>(abuf + mm[u] * APITCH + (nt * 16 + g * 4) * 2) = o;
-          }
+      for (int ks = 0; ks < 2; ++ks) {
+        const u2 lo = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][0]);
+        const u2 hi = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][1]);
+        xv[u][ks] = u4{lo[0], lo[1], hi[0], hi[1]};
       }
+      const int ay = ay0 + yl, ax = ax0 + xl;
+      keep[u] = (m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA) ? ~0u : 0u;
     }
-    __syncthreads();   // A tile complete
-
-    // conv B: 4 m-tiles x 2 n-tiles per wave, then activation -> staging
-    f4 acc[4][2];
+    f4 acc[3][NAT];
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NAT; ++nt) {
+        const f4 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[0][nt]),
+                                                             __builtin_bit_cast(h8, xv[u][0]), f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        acc[u][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[1][nt]),
+                                                            __builtin_bit_cast(h8, xv[u][1]), a, 0, 0, 0);
+      }
+#pragma unroll
+    for (int u = 0; u < 3; ++u)
+#pragma unroll
+      for (int nt = 0; nt < NAT; ++nt) {
+        typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+        float v[4];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (ACT_A == 1) v[e] = acc[u][nt][e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[u][nt][e]));
+          else v[e] = act_t<ACT_A>(acc[u][nt][e]);
+        }
+        // zero outside the image (conv B's padding): one mask per packed pair of halves
+        const u2 o = {__builtin_bit_cast(uint32_t, h2{(_Float16)v[0], (_Float16)v[1]}) & keep[u],
+                      __builtin_bit_cast(uint32_t, h2{(_Float16)v[2], (_Float16)v[3]}) & keep[u]};
+        *reinterpret_cast<u2*>(ab + mm[u] * APITCH + (nt * 16 + g * 4) * 2) = o;
+      }
+  };
+  // conv B: 4 m-tiles x 2 n-tiles per wave, taps [t0, t0 + 3)
+  auto conv_b_taps = [&](int t0, const unsigned char* ab, f4 (&acc)[4][2]) __attribute__((always_inline)) {
+    if (p.variant == 3) return;
+#pragma unroll
+    for (int tap = t0; tap < t0 + 3; ++tap) {
+      const int r = tap / 3, s = tap - r * 3;
+      u4 xa[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mb = (4 * mg + i) * 16 + li;
+        const int ty = mb / TBX, tx = mb - ty * TBX;
+        const int ap = (2 * ty + r) * TAX + (2 * tx + s);
+        xa[i] = *reinterpret_cast<const u4*>(ab + ap * APITCH + g * 16);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wfr[j][tap]),
+                                                             __builtin_bit_cast(h8, xa[i]), acc[i][j], 0, 0, 0);
+    }
+  };
+  auto conv_b_init = [&](f4 (&acc)[4][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 2; ++j) acc[i][j] = f4{bb_l[j][0], bb_l[j][1], bb_l[j][2], bb_l[j][3]};
-    if (p.variant != 3) {
-#pragma unroll
-      for (int tap = 0; tap < 9; ++tap) {
-        const int r = tap / 3, s = tap - r * 3;
-        u4 xa[4];
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-          const int mb = (4 * mg + i) * 16 + li;
-          const int ty = mb / TBX, tx = mb - ty * TBX;
-          const int ap = (2 * ty + r) * TAX + (2 * tx + s);
-          xa[i] = *reinterpret_cast<const u4*>(abuf + ap * APITCH + g * 16);
-        }
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < 2; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wfr[j][tap]),
-                                                               __builtin_bit_cast(h8, xa[i]), acc[i][j], 0, 0, 0);
-      }
-    }
+  };
+  // conv B's activation -> staging tile
+  auto conv_b_out = [&](f4 (&acc)[4][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -567,10 +558,76 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
         }
         *reinterpret_cast<h4*>(obuf + mb * CPITCH + col * 2) = o;
       }
-    pb = b;
-    poy0 = oy0;
-    pox0 = ox0;
-    __syncthreads();   // staging complete (stored at the top of the next iteration)
+  };
+  auto origin = [&](int t, int& b, int& oy0, int& ox0, int& ay0, int& ax0) {
+    tile_geom(t, b, oy0, ox0);
+    ay0 = 2 * oy0 - 1;
+    ax0 = 2 * ox0 - 1;
+  };
+
+  if constexpr (!PIPE) {
+    for (int tile = vb; tile < ntiles; tile += G) {
+      int b, oy0, ox0, ay0, ax0;
+      origin(tile, b, oy0, ox0, ay0, ax0);
+      commit();
+      if (tile + G < ntiles) prefetch(tile + G);
+      store_prev();
+      __syncthreads();   // patch of this tile in LDS; staging of the previous one read
+#pragma unroll 1
+      for (int grp = 0; grp < MA / 12; ++grp) conv_a_group(grp, abuf0, ay0, ax0);
+      __syncthreads();   // A tile complete
+      f4 acc[4][2];
+      conv_b_init(acc);
+#pragma unroll
+      for (int t0 = 0; t0 < 9; t0 += 3) conv_b_taps(t0, abuf0, acc);
+      conv_b_out(acc);
+      pb = b;
+      poy0 = oy0;
+      pox0 = ox0;
+      __syncthreads();   // staging complete (stored at the top of the next iteration)
+    }
+  } else {
+    // Software pipeline over the block's tiles, one wave per SIMD: conv B of tile t (MFMA-bound)
+    // and conv A of tile t + G (VALU-bound: its SiLU) share one instruction stream, group by group,
+    // so the SiLU issues beside conv B's MFMAs instead of in a phase of its own; A tiles are
+    // double-buffered, two barriers per tile.
+    if (vb >= ntiles) return;
+    {
+      int b, oy0, ox0, ay0, ax0;
+      origin(vb, b, oy0, ox0, ay0, ax0);
+      commit();
+      if (vb + G < ntiles) prefetch(vb + G);
+      __syncthreads();
+#pragma unroll 1
+      for (int grp = 0; grp < MA / 12; ++grp) conv_a_group(grp, abuf0, ay0, ax0);
+    }
+    int cur = 0;
+    for (int tile = vb; tile < ntiles; tile += G) {
+      int b, oy0, ox0, ay0, ax0;
+      origin(tile, b, oy0, ox0, ay0, ax0);
+      const int nxt = tile + G;
+      int nb, noy0, nox0, nay0, nax0;
+      origin(nxt < ntiles ? nxt : tile, nb, noy0, nox0, nay0, nax0);
+      if (nxt < ntiles) commit();   // the next tile's patch (its conv A runs in this iteration)
+      if (nxt + G < ntiles) prefetch(nxt + G);
+      store_prev();
+      __syncthreads();   // patch of the next tile in LDS; A tile of this one complete; staging read
+      unsigned char* ab_cur = abuf0 + cur * ABUF;
+      unsigned char* ab_nxt = abuf0 + (cur ^ 1) * ABUF;
+      f4 acc[4][2];
+      conv_b_init(acc);
+#pragma unroll
+      for (int grp = 0; grp < 3; ++grp) {
+        conv_b_taps(3 * grp, ab_cur, acc);
+        conv_a_group(grp, ab_nxt, nay0, nax0);   // (past the last tile: a harmless recompute)
+      }
+      conv_b_out(acc);
+      pb = b;
+      poy0 = oy0;
+      pox0 = ox0;
+      cur ^= 1;
+      __syncthreads();   // staging complete, next A tile complete
+    }
   }
   store_prev();
 }
@@ -591,8 +648,13 @@ hipError_t stem_t(const StemParams& p, hipStream_t st) {
   const int nblk = ntiles < cus * occ ? ntiles : cus * occ;   // persistent: blocks walk the tiles
   static const int form = [] { const char* e = getenv("YV7_STEM"); return e ? atoi(e) : 2; }();
   if constexpr (SA == 1) {   // (SA = 2, yolov7-tiny: its 10 patch pixels per thread leave stem2 one block per CU)
+    if (form == 3) {   // software-pipelined form: one block per CU
+      const int nb1 = ntiles < cus ? ntiles : cus;
+      YV7_LAUNCH((stem2_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B, true>), dim3(nb1), dim3(NT), 0, st, p);
+      return hipGetLastError();
+    }
     if (form != 1) {
-      YV7_LAUNCH((stem2_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B>), dim3(nblk), dim3(NT), 0, st, p);
+      YV7_LAUNCH((stem2_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B, false>), dim3(nblk), dim3(NT), 0, st, p);
       return hipGetLastError();
     }
   }
