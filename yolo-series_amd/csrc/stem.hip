@@ -276,8 +276,8 @@ __global__ __launch_bounds__(NT, 2) void stem_kernel(const StemParams p) {
 //   * the output staging tile has its own LDS (patch + A tile + staging = 68.6 KB, two blocks per CU),
 //     so a tile needs 3 barriers: [stores of t-1, patch of t] | conv A | conv B + staging;
 //   * both biases in registers from kernel entry (no global load inside the tile loop).
-template <typename S, int CA, int CB, int SA, int TBY, int TBX, int ACT_A, int ACT_B, bool PIPE>
-__global__ __launch_bounds__(NT, PIPE ? 1 : 2) void stem2_kernel(const StemParams p) {
+template <typename S, int CA, int CB, int SA, int TBY, int TBX, int ACT_A, int ACT_B>
+__global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
   constexpr int TAY = 2 * TBY + 1, TAX = 2 * TBX + 1;
   constexpr int PY = SA * (TAY - 1) + 3, PX = SA * (TAX - 1) + 3;
   constexpr int NA = TAY * TAX;
@@ -290,11 +290,10 @@ __global__ __launch_bounds__(NT, PIPE ? 1 : 2) void stem2_kernel(const StemParam
   constexpr int OUTB = TBY * TBX * CPITCH;
   static_assert(CB == 64 && CA == 32, "4 waves = 2 m-groups x 2 n-groups of 32 channels; one MFMA k-step per tap");
   static_assert(MB == 8 && MA % 12 == 0, "conv B: 4 m-tiles per wave; conv A: groups of 3 m-tiles per wave");
-  constexpr int NAB = PIPE ? 2 : 1;                  // A tiles in LDS (PIPE: double-buffered)
-  __shared__ __attribute__((aligned(16))) unsigned char smem[PATCH + NAB * ABUF + OUTB];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[PATCH + ABUF + OUTB];
   _Float16* patch = reinterpret_cast<_Float16*>(smem);
   unsigned char* abuf0 = smem + PATCH;
-  unsigned char* obuf = smem + PATCH + NAB * ABUF;
+  unsigned char* obuf = smem + PATCH + ABUF;
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, li = lane & 15;
@@ -565,7 +564,7 @@ __global__ __launch_bounds__(NT, PIPE ? 1 : 2) void stem2_kernel(const StemParam
     ax0 = 2 * ox0 - 1;
   };
 
-  if constexpr (!PIPE) {
+  {
     for (int tile = vb; tile < ntiles; tile += G) {
       int b, oy0, ox0, ay0, ax0;
       origin(tile, b, oy0, ox0, ay0, ax0);
@@ -585,48 +584,6 @@ __global__ __launch_bounds__(NT, PIPE ? 1 : 2) void stem2_kernel(const StemParam
       poy0 = oy0;
       pox0 = ox0;
       __syncthreads();   // staging complete (stored at the top of the next iteration)
-    }
-  } else {
-    // Software pipeline over the block's tiles, one wave per SIMD: conv B of tile t (MFMA-bound)
-    // and conv A of tile t + G (VALU-bound: its SiLU) share one instruction stream, group by group,
-    // so the SiLU issues beside conv B's MFMAs instead of in a phase of its own; A tiles are
-    // double-buffered, two barriers per tile.
-    if (vb >= ntiles) return;
-    {
-      int b, oy0, ox0, ay0, ax0;
-      origin(vb, b, oy0, ox0, ay0, ax0);
-      commit();
-      if (vb + G < ntiles) prefetch(vb + G);
-      __syncthreads();
-#pragma unroll 1
-      for (int grp = 0; grp < MA / 12; ++grp) conv_a_group(grp, abuf0, ay0, ax0);
-    }
-    int cur = 0;
-    for (int tile = vb; tile < ntiles; tile += G) {
-      int b, oy0, ox0, ay0, ax0;
-      origin(tile, b, oy0, ox0, ay0, ax0);
-      const int nxt = tile + G;
-      int nb, noy0, nox0, nay0, nax0;
-      origin(nxt < ntiles ? nxt : tile, nb, noy0, nox0, nay0, nax0);
-      if (nxt < ntiles) commit();   // the next tile's patch (its conv A runs in this iteration)
-      if (nxt + G < ntiles) prefetch(nxt + G);
-      store_prev();
-      __syncthreads();   // patch of the next tile in LDS; A tile of this one complete; staging read
-      unsigned char* ab_cur = abuf0 + cur * ABUF;
-      unsigned char* ab_nxt = abuf0 + (cur ^ 1) * ABUF;
-      f4 acc[4][2];
-      conv_b_init(acc);
-#pragma unroll
-      for (int grp = 0; grp < 3; ++grp) {
-        conv_b_taps(3 * grp, ab_cur, acc);
-        conv_a_group(grp, ab_nxt, nay0, nax0);   // (past the last tile: a harmless recompute)
-      }
-      conv_b_out(acc);
-      pb = b;
-      poy0 = oy0;
-      pox0 = ox0;
-      cur ^= 1;
-      __syncthreads();   // staging complete, next A tile complete
     }
   }
   store_prev();
@@ -648,13 +605,8 @@ hipError_t stem_t(const StemParams& p, hipStream_t st) {
   const int nblk = ntiles < cus * occ ? ntiles : cus * occ;   // persistent: blocks walk the tiles
   static const int form = [] { const char* e = getenv("YV7_STEM"); return e ? atoi(e) : 2; }();
   if constexpr (SA == 1) {   // (SA = 2, yolov7-tiny: its 10 patch pixels per thread leave stem2 one block per CU)
-    if (form == 3) {   // software-pipelined form: one block per CU
-      const int nb1 = ntiles < cus ? ntiles : cus;
-      YV7_LAUNCH((stem2_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B, true>), dim3(nb1), dim3(NT), 0, st, p);
-      return hipGetLastError();
-    }
     if (form != 1) {
-      YV7_LAUNCH((stem2_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B, false>), dim3(nblk), dim3(NT), 0, st, p);
+      YV7_LAUNCH((stem2_kernel<S, CA, CB, SA, TBY, TBX, ACT_A, ACT_B>), dim3(nblk), dim3(NT), 0, st, p);
       return hipGetLastError();
     }
   }
