@@ -376,12 +376,12 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
                  c2 = __builtin_bit_cast(h2, pre[k][2]);
         const int py = i / UPR, px = 2 * (i - py * UPR);
         if (i < PY * UPR) {
-          *reinterpret_cast<h4*>(patch + (py * PX + px) * 4) = h4{c0[0], c1[0], c2[0], (_Float16)1.f};
-          if (px + 1 < PX) *reinterpret_cast<h4*>(patch + (py * PX + px + 1) * 4) = h4{c0[1], c1[1], c2[1], (_Float16)1.f};
+          *reinterpret_cast<h4*>(patch + (py * PX + px) * 4) = h4{c0[0], c1[0], c2[0], (_Float16)0.f};
+          if (px + 1 < PX) *reinterpret_cast<h4*>(patch + (py * PX + px + 1) * 4) = h4{c0[1], c1[1], c2[1], (_Float16)0.f};
         }
       } else {
         const h4 v = {(_Float16)__builtin_bit_cast(float, pre[k][0]), (_Float16)__builtin_bit_cast(float, pre[k][1]),
-                      (_Float16)__builtin_bit_cast(float, pre[k][2]), (_Float16)1.f};
+                      (_Float16)__builtin_bit_cast(float, pre[k][2]), (_Float16)0.f};
         if (i < PY * PX) *reinterpret_cast<h4*>(patch + i * 4) = v;
       }
     }
@@ -394,10 +394,7 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
     }
     return (gg == 0 && half == 0) ? 8 : -1;
   };
-  // conv A's bias rides in the MFMA: every patch pixel's 4th channel is 1.0, and the weight slots of
-  // that channel carry the bias as two fp16 parts (tap (0,0): hi, tap (0,1): the remainder, exact to
-  // ~2^-22 of it) — the accumulators start at the inline constant 0, no bias copies per tile.  Slots
-  // with no tap (K step 1 but for tap (2,2)) read patch pixel 0 against zero weights.
+  // Slots with no tap (K step 1 but for tap (2,2)) read patch pixel 0 against zero weights.
   constexpr int NAT = CA / 16;
   u4 wa[2][NAT];
 #pragma unroll
@@ -407,15 +404,13 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
       typedef _Float16 h8v __attribute__((ext_vector_type(8)));
       h8v w8;
       const _Float16* wrow = reinterpret_cast<const _Float16*>(p.wa) + (size_t)(nt * 16 + li) * p.kpad_a;
-      const float bs = p.ba[nt * 16 + li] * sa_scale;
-      const _Float16 bhi = (_Float16)bs, blo = (_Float16)(bs - (float)bhi);
 #pragma unroll
       for (int h2 = 0; h2 < 2; ++h2) {
         const int tap = tap_of(ks, g, h2);
 #pragma unroll
         for (int ci = 0; ci < 3; ++ci)
           w8[h2 * 4 + ci] = tap >= 0 ? (_Float16)((float)wrow[tap * 3 + ci] * sa_scale) : (_Float16)0.f;
-        w8[h2 * 4 + 3] = tap == 0 ? bhi : tap == 1 ? blo : (_Float16)0.f;
+        w8[h2 * 4 + 3] = (_Float16)0.f;
       }
       wa[ks][nt] = __builtin_bit_cast(u4, w8);
     }
@@ -427,6 +422,11 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
       const int tap = tap_of(ks, g, h2);
       toff[ks][h2] = tap >= 0 ? ((tap / 3) * PX + tap % 3) * 8 : 0;
     }
+  float ba_l[NAT][4];   // conv A's bias (scaled like its weights) as the accumulators' start
+#pragma unroll
+  for (int nt = 0; nt < NAT; ++nt)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) ba_l[nt][e] = p.ba[nt * 16 + g * 4 + e] * sa_scale;
 
   const int G = gridDim.x;
   const int vb = G % 8 == 0 ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
@@ -486,8 +486,8 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
     for (int u = 0; u < 3; ++u)
 #pragma unroll
       for (int nt = 0; nt < NAT; ++nt) {
-        const f4 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[0][nt]),
-                                                             __builtin_bit_cast(h8, xv[u][0]), f4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
+        const f4 a = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[0][nt]), __builtin_bit_cast(h8, xv[u][0]),
+                                                             f4{ba_l[nt][0], ba_l[nt][1], ba_l[nt][2], ba_l[nt][3]}, 0, 0, 0);
         acc[u][nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[1][nt]),
                                                             __builtin_bit_cast(h8, xv[u][1]), a, 0, 0, 0);
       }
