@@ -148,17 +148,8 @@ __device__ __forceinline__ int swz_bk(int row, int chunk) {
 constexpr int det_tab(int BM, int BN) { return BM * BN * 4; }
 constexpr int det_lds(int BM, int BN) { return det_tab(BM, BN) + BM * 16 + 64; }
 
-// The head's sigmoid rcp(1 + 2^(-log2(e) v)) of 4 accumulators, the multiply and add on packed pairs
-__device__ __forceinline__ f4 det_sig4(f4 v) {
-  f4 r;
-#pragma unroll
-  for (int h = 0; h < 2; ++h) {
-    const f2 z = f2{v[2 * h], v[2 * h + 1]} * -1.4426950408889634f;
-    const f2 t = f2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + 1.0f;
-    r[2 * h] = __builtin_amdgcn_rcpf(t.x);
-    r[2 * h + 1] = __builtin_amdgcn_rcpf(t.y);
-  }
-  return r;
+__device__ __forceinline__ float det_sig(float v) {
+  return __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
 }
 
 struct DetTab {
@@ -230,12 +221,11 @@ __device__ __forceinline__ void det_stage(const ConvParams& p, unsigned char* sm
     for (int i = 0; i < TM; ++i) {
       const int row = wm * WTM + i * 16 + li;
       const int roff = row * NO;
-      const f4 sg = det_sig4(acc[j][i]);
       if (dec) {
         const float gxv = t.gx[row], gyv = t.gy[row];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const float s = sg[e];
+          const float s = det_sig(acc[j][i][e]);
           const float t2 = s * 2.0f;
           const float xy = (t2 - 0.5f + (co[e] == 0 ? gxv : gyv)) * p.stride;
           const float wh = (t2 * t2) * anc_wh[e];
@@ -243,7 +233,7 @@ __device__ __forceinline__ void det_stage(const ConvParams& p, unsigned char* sm
         }
       } else {
 #pragma unroll
-        for (int e = 0; e < 4; ++e) zs[zoff[e] + (live[e] ? roff : 0)] = sg[e];
+        for (int e = 0; e < 4; ++e) zs[zoff[e] + (live[e] ? roff : 0)] = det_sig(acc[j][i][e]);
       }
     }
   }

@@ -497,18 +497,10 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
       for (int nt = 0; nt < NAT; ++nt) {
         typedef _Float16 h2 __attribute__((ext_vector_type(2)));
         float v[4];
-        if constexpr (ACT_A == 1) {   // z * rcp(1 + 2^z), the adds and multiplies on packed pairs
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const f2 z = {acc[u][nt][2 * h], acc[u][nt][2 * h + 1]};
-            const f2 t = f2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + 1.0f;
-            const f2 r = z * f2{__builtin_amdgcn_rcpf(t.x), __builtin_amdgcn_rcpf(t.y)};
-            v[2 * h] = r.x;
-            v[2 * h + 1] = r.y;
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) v[e] = act_t<ACT_A>(acc[u][nt][e]);
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (ACT_A == 1) v[e] = acc[u][nt][e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[u][nt][e]));
+          else v[e] = act_t<ACT_A>(acc[u][nt][e]);
         }
         // zero outside the image (conv B's padding): one mask per packed pair of halves
         const u2 o = {__builtin_bit_cast(uint32_t, h2{(_Float16)v[0], (_Float16)v[1]}) & keep[u],
@@ -554,18 +546,14 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
         const int col = (2 * ng + j) * 16 + g * 4;
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         h4 o;
-        if constexpr (ACT_A == 1 && ACT_B == 1) {   // (z * -ln2) * rcp(1 + 2^z) on packed pairs
 #pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const f2 z = {acc[i][j][2 * h], acc[i][j][2 * h + 1]};
-            const f2 t = f2{__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)} + 1.0f;
-            const f2 r = (z * -0.6931471805599453f) * f2{__builtin_amdgcn_rcpf(t.x), __builtin_amdgcn_rcpf(t.y)};
-            o[2 * h] = (_Float16)r.x;
-            o[2 * h + 1] = (_Float16)r.y;
-          }
-        } else {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = (_Float16)act_t<ACT_B>(acc[i][j][e] / sb_scale);
+        for (int e = 0; e < 4; ++e) {
+          float v;
+          if constexpr (ACT_A == 1 && ACT_B == 1)
+            v = (acc[i][j][e] * -0.6931471805599453f) * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[i][j][e]));
+          else
+            v = act_t<ACT_B>(acc[i][j][e] / sb_scale);
+          o[e] = (_Float16)v;
         }
         *reinterpret_cast<h4*>(obuf + mb * CPITCH + col * 2) = o;
       }
