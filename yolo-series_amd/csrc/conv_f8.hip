@@ -234,17 +234,10 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * ROWB8 <= 76 * 1
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         typedef uint32_t u2 __attribute__((ext_vector_type(2)));
         h4 va, vb;
-        f4 xa, xb;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          xa[e] = __builtin_fmaf(acc[2 * mp][ii][e], sc[2 * mp][e], bi[2 * mp][e]);
-          xb[e] = __builtin_fmaf(acc[2 * mp + 1][ii][e], sc[2 * mp + 1][e], bi[2 * mp + 1][e]);
-        }
-        const f4 fa_ = act4<ACT>(xa), fb_ = act4<ACT>(xb);   // packed-pair arithmetic, same bits as act_t
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          va[e] = (_Float16)fa_[e];
-          vb[e] = (_Float16)fb_[e];
+          va[e] = (_Float16)act_t<ACT>(__builtin_fmaf(acc[2 * mp][ii][e], sc[2 * mp][e], bi[2 * mp][e]));
+          vb[e] = (_Float16)act_t<ACT>(__builtin_fmaf(acc[2 * mp + 1][ii][e], sc[2 * mp + 1][e], bi[2 * mp + 1][e]));
         }
         const u2 a = __builtin_bit_cast(u2, va), bq = __builtin_bit_cast(u2, vb);
         const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], bq[0], false, false);
