@@ -559,9 +559,8 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
         const int row = wm * WTM + i * 16 + li;
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         h4 v;
-        const f4 fa_ = act4<ACT>(acc[j][i]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (_Float16)fa_[e];
+        for (int e = 0; e < 4; ++e) v[e] = (_Float16)act_t<ACT>(acc[j][i][e]);
         *reinterpret_cast<h4*>(Cs + row * CPITCH + col * 2) = v;
       }
     }
@@ -804,9 +803,8 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
         const int row = wm * WTM + i * 16 + li;
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         h4 v;
-        const f4 fa_ = act4<ACT>(acc[j][i]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (_Float16)fa_[e];
+        for (int e = 0; e < 4; ++e) v[e] = (_Float16)act_t<ACT>(acc[j][i][e]);
         *reinterpret_cast<h4*>(Cs + row * CPITCH + col * 2) = v;
       }
     }
@@ -981,11 +979,10 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         typedef uint32_t u2 __attribute__((ext_vector_type(2)));
         h4 va, vb;
-        const f4 fa_ = act4<ACT>(acc[2 * mp][ii]), fb_ = act4<ACT>(acc[2 * mp + 1][ii]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          va[e] = (_Float16)fa_[e];
-          vb[e] = (_Float16)fb_[e];
+          va[e] = (_Float16)act_t<ACT>(acc[2 * mp][ii][e]);
+          vb[e] = (_Float16)act_t<ACT>(acc[2 * mp + 1][ii][e]);
         }
         const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
         const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
@@ -1190,11 +1187,10 @@ __global__ __launch_bounds__(64 * WM * WN, (2 * (BM + BN) * 128 <= 76 * 1024) ? 
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         typedef uint32_t u2 __attribute__((ext_vector_type(2)));
         h4 va, vb;
-        const f4 fa_ = act4<ACT>(acc[2 * mp][ii]), fb_ = act4<ACT>(acc[2 * mp + 1][ii]);
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          va[e] = (_Float16)fa_[e];
-          vb[e] = (_Float16)fb_[e];
+          va[e] = (_Float16)act_t<ACT>(acc[2 * mp][ii][e]);
+          vb[e] = (_Float16)act_t<ACT>(acc[2 * mp + 1][ii][e]);
         }
         const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
         const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
@@ -1458,11 +1454,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
             a0 = seg_sum(a0, ((hb * 2 + 0) * 2 + ha) * 4 + i);
             a1 = seg_sum(a1, ((hb * 2 + 1) * 2 + ha) * 4 + i);
           }
-          const f4 fa_ = act4<ACT>(a0), fb_ = act4<ACT>(a1);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            va[e] = (_Float16)fa_[e];
-            vb[e] = (_Float16)fb_[e];
+            va[e] = (_Float16)act_t<ACT>(a0[e]);
+            vb[e] = (_Float16)act_t<ACT>(a1[e]);
           }
           const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
           const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
@@ -1809,11 +1804,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
           typedef _Float16 h4 __attribute__((ext_vector_type(4)));
           typedef uint32_t u2 __attribute__((ext_vector_type(2)));
           h4 va, vb;
-          const f4 fa_ = act4<ACT>(acc[h][2 * mp][i]), fb_ = act4<ACT>(acc[h][2 * mp + 1][i]);
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
-            va[e] = (_Float16)fa_[e];
-            vb[e] = (_Float16)fb_[e];
+            va[e] = (_Float16)act_t<ACT>(acc[h][2 * mp][i][e]);
+            vb[e] = (_Float16)act_t<ACT>(acc[h][2 * mp + 1][i][e]);
           }
           const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
           const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);

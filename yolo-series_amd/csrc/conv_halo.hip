@@ -185,9 +185,8 @@ __global__ __launch_bounds__(NT, 2) void conv3x3_halo_kernel(const ConvParams p)
         const int px = (wave * TM + i) * TS + li;
         typedef _Float16 h4 __attribute__((ext_vector_type(4)));
         h4 v;
-        const f4 fa_ = act4<ACT>(acc[j][i]);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) v[e] = (_Float16)fa_[e];
+        for (int e = 0; e < 4; ++e) v[e] = (_Float16)act_t<ACT>(acc[j][i][e]);
         *reinterpret_cast<h4*>(Cs + px * CPITCH + col * 2) = v;
       }
     }

@@ -190,11 +190,10 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     const int i = q >> 1, m = q & 1;
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     h4 va, vb;
-    const f4 fa_ = act4<ACT>(acc[2 * m][i]), fb_ = act4<ACT>(acc[2 * m + 1][i]);
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      va[e] = (_Float16)fa_[e];
-      vb[e] = (_Float16)fb_[e];
+      va[e] = (_Float16)act_t<ACT>(acc[2 * m][i][e]);
+      vb[e] = (_Float16)act_t<ACT>(acc[2 * m + 1][i][e]);
     }
     const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
     const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);

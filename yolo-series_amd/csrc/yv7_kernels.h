@@ -65,26 +65,6 @@ __device__ __forceinline__ float act_t(float v) {
   return v;
 }
 
-// act_t on 4 accumulators, the plain arithmetic as packed fp32 (v_pk_mul_f32 / v_pk_add_f32: two
-// lanes' worth per instruction; per element the same IEEE operations as act_t, so the same bits)
-typedef float f2 __attribute__((ext_vector_type(2)));
-template <int ACT>
-__device__ __forceinline__ f2 act2(f2 v) {
-  if constexpr (ACT == 1) {
-    const f2 z = v * -1.4426950408889634f;
-    f2 t = {__builtin_amdgcn_exp2f(z.x), __builtin_amdgcn_exp2f(z.y)};
-    t = t + 1.0f;
-    return v * f2{__builtin_amdgcn_rcpf(t.x), __builtin_amdgcn_rcpf(t.y)};
-  } else {
-    return f2{act_t<ACT>(v.x), act_t<ACT>(v.y)};
-  }
-}
-template <int ACT>
-__device__ __forceinline__ f4 act4(f4 v) {
-  const f2 lo = act2<ACT>(f2{v[0], v[1]}), hi = act2<ACT>(f2{v[2], v[3]});
-  return f4{lo.x, lo.y, hi.x, hi.y};
-}
-
 // Calls f(std::integral_constant<int, ACT>) with the layer's activation as a compile-time constant, so
 // an epilogue is straight-line code (a runtime switch per element costs more than the SiLU itself).
 template <typename F>
