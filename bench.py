@@ -8,10 +8,13 @@ Weights: seeded synthetic yolov7 weights (no checkpoints offline), packed once o
 RCCL-broadcast.  N > 1 is launched by torch.distributed.run, one process per GPU; per-GPU work is
 fixed (weak scaling); value = all images processed / max-over-ranks wall time of the K timed steps.
 
-roofline: the dominant kernel is the implicit-GEMM conv (CONV/DETECT launches, ~90 % of GPU time).
-Its per-launch time is measured live with HIP events recorded by libyv7 around every op of the first
-two timed forwards (on the forward's own stream); achieved = algorithmic HBM bytes per conv launch
-(layer-boundary model) / mean conv launch time, against 8 TB/s.
+roofline: per kernel instantiation (the kernels the dispatch picks, yv7_op_kernels): launches, mean
+serial launch time (HIP event pairs on each op's own dispatches, two forwards after the timed region,
+every kernel alone on the chip — the durations a rocprofv3 kernel trace of a serial forward reports),
+algorithmic bytes and FLOPs per launch (layer-boundary model) and roof = max(bytes / 8 TB/s,
+FLOPs / 2.5 PF); `frac` is the dominant kernel's (most time per forward) achieved / peak on its
+binding roof.  The whole job against the layer-boundary HBM ceiling is `job_frac`; the conv family's
+bytes over the timed region as a whole `family_stream_frac`.
 cpu_baseline: the oracle (CPU restatement of the reference detect.py path: torch CPU fp32 NCHW +
 restated NMS), rank 0 only, on a bounded sample of the same workload.
 """
@@ -32,9 +35,7 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # HBM bytes per conv launch from PMC counters of this same workload (scripts/pmc_traffic.sh: separate
 # FETCH_SIZE / WRITE_SIZE rocprofv3 passes; scripts/pmc_traffic.py: x2 FETCH correction for gfx950)
-PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r2_pmc_traffic.json')
-if not os.path.exists(PMC_TRAFFIC):
-    PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r1_pmc_traffic.json')
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r3_pmc_traffic.json')   # per kernel (scripts/pmc_traffic_kernels.py)
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA
 
 
@@ -71,6 +72,9 @@ def parse(argv=None):
                     'batch as uint8 frames from pinned host memory (PCIe-inclusive rate)')
     ap.add_argument('--graph', action='store_true', help='replay the step as a HIP graph (measured: same speed '
                     'as eager launches on MI355X, the inter-kernel gaps are dependency drains, not launch cost)')
+    ap.add_argument('--inputs', type=int, default=4, help='distinct resident input batches the steps rotate '
+                    'through (4 x 78.6 MB fp16 at bs32 640: more than the 256 MiB Infinity Cache holds)')
+    ap.add_argument('--map-frames', type=int, default=16, help='frames of the mAP@0.5 parity sample')
     return ap.parse_args(argv)
 
 
@@ -122,10 +126,21 @@ def plumbing(a):
     ok = same and gc.tolist() == list(range(a.batch * world)) and gd.shape[0] == a.batch * world
     flags = torch.tensor([int(ok)])
     dist.all_reduce(flags, op=dist.ReduceOp.MIN)
+    # the fields the GPU run reports per rank (here on gloo): the all-gather's time per batch and the
+    # world size each rank's process group saw
+    t0 = time.perf_counter()
+    for _ in range(10):
+        ydist.gather_detections(det, src, cnt)
+    us = (time.perf_counter() - t0) / 10 * 1e6
+    per = torch.tensor([us, float(dist.get_world_size())], dtype=torch.float64)
+    pl = [torch.zeros_like(per) for _ in range(world)]
+    dist.all_gather(pl, per)
     if rank == 0:
         print(json.dumps({'plumbing': True, 'n_gpus': world, 'world_size_seen': world, 'backend': 'gloo',
                           'weights_broadcast_bytes': int(blob.numel()), 'global_batch': a.batch * world,
-                          'all_ranks_ok': bool(flags.item())}), flush=True)
+                          'all_ranks_ok': bool(flags.item()),
+                          'allgather_us_per_batch': [round(float(v[0]), 1) for v in pl],
+                          'per_rank_world_size_seen': [int(v[1]) for v in pl]}), flush=True)
     dist.barrier()
     dist.destroy_process_group()
 
@@ -149,7 +164,7 @@ def _cpu_quota():
         return None
 
 
-def cpu_baseline(model_name, img, seconds, plan=None, dev=None, parity_frames=4, big_batch=32):
+def cpu_baseline(model_name, img, seconds, plan=None, dev=None, parity_frames=16, big_batch=32):
     """The oracle (reference CPU path restated) on the host cores this job may use: forward + NMS,
     timed separately like detect.py:142-153 (t2 - t1 forward, t3 - t2 NMS), at batch 1 (detect.py's
     loop; `value`) for about `seconds`, and one batch of `big_batch` frames (test.py's batch size).
@@ -260,7 +275,11 @@ def main(argv=None):
 
     B, H, W = a.batch, a.img, a.img
     g = torch.Generator(device=dev).manual_seed(1000 + rank)
-    x = (torch.randint(0, 256, (B, 3, H, W), generator=g, device=dev, dtype=torch.uint8).to(dt) / 255.0)
+    # a.inputs distinct resident batches, step k reads batch k % a.inputs (together larger than the
+    # Infinity Cache: the input read is a real HBM read, as for a stream of new frames)
+    xin = [(torch.randint(0, 256, (B, 3, H, W), generator=g, device=dev, dtype=torch.uint8).to(dt) / 255.0)
+           for _ in range(max(1, a.inputs))]
+    x = xin[0]
     N = plan.num_rows(H, W)
     # Serving pipeline: batch k's NMS (and on multi-GPU its detection all-gather) runs on a second HIP
     # stream while batch k+1's forward runs on the first, so z / row records / detections are double
@@ -301,7 +320,7 @@ def main(argv=None):
     sub = B // nsplit
     streams = [torch.cuda.current_stream(dev)] + [torch.cuda.Stream(dev) for _ in range(nsplit - 1)]
 
-    def forward(z, rowbest):
+    def forward(z, rowbest, x):
         if nsplit == 1:
             plan.forward_into(x, z, rowbest=rowbest)
             return
@@ -321,10 +340,11 @@ def main(argv=None):
 
     def step():
         k = nstep[0] % nbuf
+        xk = xin[nstep[0] % len(xin)]
         nstep[0] += 1
         if runner is not None:
             if h2d is None:
-                runner.submit(x)
+                runner.submit(xk)
                 return
             # --h2d: this batch's uint8 frames come from pinned host memory (detect.py:100-104 hands the
             # model host frames): upload + /255 on the default stream, ordered after the forward that
@@ -338,13 +358,13 @@ def main(argv=None):
             runner.submit(h2d['x'][j])
             return
         if not pipeline:
-            forward(zs[k], rowbests[k])
+            forward(zs[k], rowbests[k], xk)
             post(k)
             return
         main = torch.cuda.current_stream(dev)
         if nstep[0] > nbuf:
             main.wait_event(nms_done[k])      # the NMS that read buffer k two batches ago has finished
-        forward(zs[k], rowbests[k])
+        forward(zs[k], rowbests[k], xk)
         fwd_done[k].record(main)
         nms_stream.wait_event(fwd_done[k])
         with torch.cuda.stream(nms_stream):
@@ -391,13 +411,18 @@ def main(argv=None):
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
-    if distributed:
+    rank_elapsed = [elapsed]
+    if distributed:   # every rank's own time (per-rank img/s), then the job's: the slowest rank
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        tl = [torch.zeros_like(t) for _ in range(dist.get_world_size())]
+        dist.all_gather(tl, t)
+        rank_elapsed = [float(v.item()) for v in tl]
+        elapsed = max(rank_elapsed)
 
     from yv7 import _lib as L
+    from yv7.runtime import kernel_key
     costs = plan.op_costs(B, H, W, x_bytes=x.element_size(), with_raw=False)
+    kernels = plan.op_kernels(B, H, W)
 
     def conv_family(nf, op_ms):
         """(mean conv/DETECT launch s, bytes per launch, flops per launch, launches, forward ms, conv ms)."""
@@ -412,11 +437,39 @@ def main(argv=None):
         return (max(conv_ms / 1e3 / nconv, 1e-12), conv_bytes / nconv, conv_flops / nconv, nconv,
                 sum(op_ms) / max(nf, 1), conv_ms)
 
+    def kernel_table(nf, op_ms):
+        """Per kernel instantiation (the op's main kernel: its last launch): launches per forward,
+        mean launch us, algorithmic bytes / FLOPs per launch, roof us = max(bytes / 8 TB/s, FLOPs / 2.5
+        PF), frac = roof / time, the binding roof."""
+        fam = {}
+        for i, ((kind, fl, by), ms) in enumerate(zip(costs, op_ms)):
+            if not kernels[i]:
+                continue
+            k = kernel_key(kernels[i][-1])
+            f = fam.setdefault(k, {'kernel': k, 'launches': 0, 'ms': 0.0, 'bytes': 0.0, 'flops': 0.0, 'ops': []})
+            f['launches'] += 1
+            f['ms'] += ms / max(nf, 1)
+            f['bytes'] += by
+            f['flops'] += fl
+            f['ops'].append(i)
+        out = []
+        for f in sorted(fam.values(), key=lambda f: -f['ms']):
+            n = f['launches']
+            us = f['ms'] * 1e3 / n
+            hb, mf = f['bytes'] / n / (HBM_PEAK_GBS * 1e9) * 1e6, f['flops'] / n / (MFMA_F16_PEAK_TFLOPS * 1e12) * 1e6
+            out.append({'kernel': f['kernel'], 'launches_per_forward': n, 'us_per_launch': round(us, 2),
+                        'bytes_per_launch': round(f['bytes'] / n), 'flops_per_launch': round(f['flops'] / n),
+                        'roof_us': round(max(hb, mf), 2), 'bound': 'hbm' if hb >= mf else 'mfma',
+                        'frac': round(max(hb, mf) / us, 4) if us > 0 else None,
+                        'share_of_forward': round(f['ms'] / max(sum(op_ms) / max(nf, 1), 1e-12), 4), 'ops': f['ops']})
+        return out
+
     nf, op_ms = plan.profile_read()
     timed = conv_family(nf, op_ms)
+    live_table = kernel_table(nf, op_ms) if nf else []
     # Diagnostics after the timed region (never `value`): two serial forwards with per-op events (each
-    # kernel alone on the chip), then detect.py's split (detect.py:142-153): forward and NMS timed apart
-    # with HIP events on one stream, one batch at a time.
+    # kernel alone on the chip) — the roofline's per-kernel launch times — then detect.py's split
+    # (detect.py:142-153): forward and NMS timed apart with HIP events on one stream, one batch at a time.
     plan.profile_enable(2)
     for _ in range(2):
         plan.forward_into(x, z, rowbest=rowbest)
@@ -424,6 +477,7 @@ def main(argv=None):
     nf_s, op_ms_s = plan.profile_read()
     plan.profile_enable(0)
     serial = conv_family(nf_s, op_ms_s)
+    table = kernel_table(nf_s, op_ms_s)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     f_ms = n_ms = 0.0
     for _ in range(3):
@@ -435,9 +489,43 @@ def main(argv=None):
         ev[2].synchronize()
         f_ms += ev[0].elapsed_time(ev[1]) / 3
         n_ms += ev[1].elapsed_time(ev[2]) / 3
+    # NMS workload: candidates per image (rows passing obj > conf and best obj*cls > conf, general.py:653,
+    # 684), and the NMS at a lighter threshold, where nms_fast runs to the end of its candidate list
+    # instead of stopping at max_det (general.py:705-706)
+    nms_load = {}
+    for conf in (0.25, 0.5):
+        cand = ((rowbest[..., 0] > conf) & (rowbest[..., 1] > conf)).sum(1).float()
+        nms_batched(z, conf, 0.45, out=(det, src, cnt), rowbest=rowbest)
+        torch.cuda.synchronize()
+        ms = 0.0
+        for _ in range(5):
+            ev[0].record()
+            nms_batched(z, conf, 0.45, out=(det, src, cnt), rowbest=rowbest)
+            ev[1].record()
+            ev[1].synchronize()
+            ms += ev[0].elapsed_time(ev[1]) / 5
+        nms_load[f'conf_{conf}'] = {'candidates_per_image': round(float(cand.mean()), 1),
+                                    'candidates_min_max': [int(cand.min()), int(cand.max())],
+                                    'dets_per_image': round(float(cnt.float().mean()), 1),
+                                    'nms_ms_per_batch': round(ms, 4)}
+    # multi-GPU: the per-batch detection all-gather alone (the collective the bench issues every step)
+    gather_us = None
+    if distributed:
+        dist.barrier()
+        for _ in range(3):
+            ydist.gather_detections(det, src, cnt, force=force_dist)
+        torch.cuda.synchronize()
+        ev[0].record()
+        for _ in range(20):
+            ydist.gather_detections(det, src, cnt, force=force_dist)
+        ev[1].record()
+        ev[1].synchronize()
+        gather_us = round(ev[0].elapsed_time(ev[1]) / 20 * 1e3, 1)
+        gt = torch.tensor([gather_us], device=dev, dtype=torch.float64)
+        gl = [torch.zeros_like(gt) for _ in range(dist.get_world_size())]
+        dist.all_gather(gl, gt)
+        gather_us = [float(v.item()) for v in gl]
     mean_launch_s, bytes_per_launch, flops_per_launch, nconv, fwd_ms, conv_ms = timed if nf else serial
-    achieved_gbs = bytes_per_launch / mean_launch_s / 1e9
-    achieved_tf = flops_per_launch / mean_launch_s / 1e12
     # whole-job ceiling: SURVEY §8d's canonical layer-boundary bytes per image (reference module boundaries,
     # weights once per batch) at 8 TB/s; other configs: the plan's own op costs (which already credit the
     # sibling-GEMM merges, so they slightly overstate that ceiling)
@@ -445,10 +533,23 @@ def main(argv=None):
     img_bytes = canon.get((a.model, H, a.dtype), sum(by for _, _, by in costs) / B)
     job_ceiling = HBM_PEAK_GBS * 1e9 / img_bytes   # images/s per GPU
     count_mean = float((runner.cnt[0] if runner is not None else cnt).float().mean().item())
+    # the dominant kernel (most serial time per forward): achieved / peak on its binding roof
+    dom = table[0]
+    if dom['bound'] == 'hbm':
+        ach, peak, unit = dom['bytes_per_launch'] / dom['us_per_launch'] / 1e3, HBM_PEAK_GBS, 'GB/s'
+    else:
+        ach, peak, unit = dom['flops_per_launch'] / dom['us_per_launch'] / 1e6, MFMA_F16_PEAK_TFLOPS, 'TFLOP/s'
     traffic = None
-    if a.model == 'yolov7' and B == 32 and H == 640 and a.dtype == 'f16' and os.path.exists(PMC_TRAFFIC):
+    traffic_src = None
+    if os.path.exists(PMC_TRAFFIC):
         with open(PMC_TRAFFIC) as f:
-            traffic = round(json.load(f)['conv_family']['hbm_bytes_per_launch'])
+            tj = json.load(f)
+        cfg = tj.get('workload', {})
+        if cfg.get('model', 'yolov7') == a.model and cfg.get('batch', 32) == B and cfg.get('img', 640) == H \
+                and cfg.get('dtype', 'f16') == a.dtype and dom['kernel'] in tj.get('kernels', {}):
+            traffic = round(tj['kernels'][dom['kernel']]['hbm_bytes_per_launch'])
+            traffic_src = f'profiles/{os.path.basename(PMC_TRAFFIC)} ({tj.get("tree", "")})'
+    dispatch_env = {k: v for k, v in sorted(os.environ.items()) if k.startswith('YV7_')}
 
     if rank == 0:
         value = world * B * a.steps / elapsed
@@ -470,45 +571,52 @@ def main(argv=None):
                                    + (' + RCCL all-gather of detections' if distributed else ''),
                        'global_batch': world * B, 'img': H, 'parallelism': f'dp{world}',
                        'rccl_world_size': dist.get_world_size() if distributed else 1,
-                       'weights': 'seeded synthetic, RCCL-broadcast' if distributed else 'seeded synthetic'},
-            'roofline': {'bound': 'hbm', 'achieved': round(achieved_gbs, 1), 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-                         'frac': round(achieved_gbs / HBM_PEAK_GBS, 4), 'traffic': traffic,
-                         'traffic_unit': f'bytes per launch (PMC, profiles/{os.path.basename(PMC_TRAFFIC)})',
-                         'kernel': 'conv kernels (MFMA implicit-GEMM ring / persistent ring / weight-stationary '
-                                   '3x3 / halo; all CONV and DETECT launches of the forward)',
-                         'launches_per_forward': nconv, 'mean_launch_us': round(mean_launch_s * 1e6, 2),
-                         'timing': (f'HIP event pair on every op\'s own kernel dispatches (hipExtLaunchKernel: '
-                                    f'dispatch begin .. end, as rocprofv3 reports) for {nf} forwards inside the '
-                                    f'timed region ({nstreams} stream(s) in flight)') if nf else
-                                   'HIP event pairs on every op of 2 serial forwards after the timed region',
-                         'algorithmic_bytes_per_launch': round(bytes_per_launch),
-                         'mfma_tflops': round(achieved_tf, 1),
-                         'mfma_frac': round(achieved_tf / MFMA_F16_PEAK_TFLOPS, 4),
-                         # whole job: images/s against the layer-boundary HBM ceiling of the whole forward
-                         # (17 625 img/s for yolov7 640 bs32 fp16)
+                       'weights': 'seeded synthetic, RCCL-broadcast' if distributed else 'seeded synthetic',
+                       'resident_input_batches': len(xin), 'dispatch_env': dispatch_env},
+            'roofline': {'bound': dom['bound'], 'achieved': round(ach, 1), 'peak': peak, 'unit': unit,
+                         'frac': round(ach / peak, 4), 'traffic': traffic,
+                         'traffic_unit': 'HBM bytes per launch of this kernel (PMC: 2 x FETCH_SIZE + WRITE_SIZE, '
+                                         'separate passes of a serial forward)', 'traffic_source': traffic_src,
+                         'kernel': dom['kernel'], 'launches_per_forward': dom['launches_per_forward'],
+                         'mean_launch_us': dom['us_per_launch'],
+                         'algorithmic_bytes_per_launch': dom['bytes_per_launch'],
+                         'algorithmic_flops_per_launch': dom['flops_per_launch'],
+                         'timing': 'HIP event pair on each op\'s own kernel dispatches (hipExtLaunchKernel: '
+                                   'dispatch begin .. end, as a rocprofv3 kernel trace reports), 2 serial '
+                                   'forwards after the timed region, kernels grouped by the instantiation the '
+                                   'dispatch picks (yv7_op_kernels)',
+                         'kernels_top5': [{k: v for k, v in r.items() if k != 'ops'} for r in table[:5]],
+                         # the whole job against the layer-boundary HBM ceiling of the forward (SURVEY §8d:
+                         # 17 625 img/s for yolov7 640 bs32 fp16)
                          'job_ceiling_images_per_s': round(job_ceiling, 1),
                          'job_frac': round(value / world / job_ceiling, 4),
-                         # the same family over the timed region as a whole: its algorithmic bytes per
-                         # step / ms_per_step.  With S batches in flight a launch shares the chip with
-                         # the other streams' launches, so per-launch durations (`achieved`) count
-                         # overlapped time S-fold at most; `overlap` = summed launch time / step time
+                         # all CONV / DETECT launches over the timed region as a whole: their
+                         # algorithmic bytes per step / ms_per_step
                          'family_stream_gbs': round(nconv * bytes_per_launch / (elapsed / a.steps) / 1e9, 1),
                          'family_stream_frac': round(nconv * bytes_per_launch / (elapsed / a.steps) / 1e9
-                                                     / HBM_PEAK_GBS, 4),
-                         'overlap': round(conv_ms / 1e3 / (elapsed / a.steps), 2) if nf else None},
-            'detail': {'forward_ms_events': round(fwd_ms, 3), 'conv_ms_events': round(conv_ms, 3),
+                                                     / HBM_PEAK_GBS, 4)},
+            'detail': {'serial_forward_ms': round(serial[4], 3),
                        'serial_conv_launch_us': round(serial[0] * 1e6, 2),
-                       'serial_conv_frac': round(serial[1] / serial[0] / 1e9 / HBM_PEAK_GBS, 4),
                        'serial_conv_tflops': round(serial[2] / serial[0] / 1e12, 1),
-                       'serial_forward_ms': round(serial[4], 3),
+                       'serial_sum_of_roofs_ms': round(sum(r['roof_us'] * r['launches_per_forward'] for r in table) / 1e3, 3),
+                       'live_contended': {'forwards': nf, 'forward_ms_events': round(fwd_ms, 3) if nf else None,
+                                          'conv_launch_us': round(timed[0] * 1e6, 2) if nf else None,
+                                          'overlap': round(conv_ms / 1e3 / (elapsed / a.steps), 2) if nf else None,
+                                          'note': f'event pairs on every op of {nf} forwards inside the timed region '
+                                                  f'({nstreams} stream(s) in flight: launches share the chip)'},
                        'detect_py_split_ms': {'forward': round(f_ms, 3), 'nms': round(n_ms, 3),
                                               'note': 'one batch at a time on one stream, HIP events '
                                                       '(detect.py:142-153 t2-t1 / t3-t2)'},
-                       'mean_dets_per_image': round(count_mean, 1), 'rows_per_image': N,
-                       'profiled_forwards': nf, 'nms_overlapped_with_next_forward': pipeline or nstreams > 1, 'hip_graph': graph is not None, 'sub_batches': nsplit, 'streams': nstreams, 'h2d_uint8_frames': bool(a.h2d)},
+                       'mean_dets_per_image': round(count_mean, 1), 'rows_per_image': N, 'nms_load': nms_load,
+                       'nms_overlapped_with_next_forward': pipeline or nstreams > 1, 'hip_graph': graph is not None,
+                       'sub_batches': nsplit, 'streams': nstreams, 'h2d_uint8_frames': bool(a.h2d)},
         }
+        if distributed:
+            res['detail']['per_rank_images_per_s'] = [round(B * a.steps / t_, 1) for t_ in rank_elapsed]
+            res['detail']['allgather_us_per_batch'] = gather_us
         if not a.no_cpu_baseline and world == 1:
-            res['cpu_baseline'] = cpu_baseline(a.model, a.img, a.cpu_seconds, plan=plan, dev=dev)
+            res['cpu_baseline'] = cpu_baseline(a.model, a.img, a.cpu_seconds, plan=plan, dev=dev,
+                                               parity_frames=a.map_frames)
             if 'map_parity' in res['cpu_baseline']:
                 res['map50_parity'] = res['cpu_baseline']['map_parity']['map50']
         print(json.dumps(res), flush=True)

@@ -143,6 +143,12 @@ typedef struct {
 int yv7_forward(yv7_plan* plan, const void* x, int x_dtype, int B, int H, int W, float* z_out,
                 float* raw_out, yv7_row_best* rowbest_out, void* workspace, size_t ws_bytes, void* stream);
 
+/* The kernels the dispatch launches for every op of a [B,3,H,W] forward, without running it (a dry
+ * run of yv7_forward's op loop): one line per op, "op<TAB>kernel[|kernel...]", kernel = the demangled
+ * symbol rocprofv3's kernel trace reports.  Lets a caller attribute per-op timings (yv7_profile_read)
+ * to kernel families.  Needs the plan's device to be current; buf receives a NUL-terminated string. */
+int yv7_op_kernels(yv7_plan* plan, int B, int H, int W, char* buf, size_t bytes);
+
 /* Force the kernel configuration of one CONV / DETECT op (0 = the tuned dispatch, the default).  For
  * parity tests of every kernel variant and A/B timing; the accepted values are the real kernel
  * configurations of the fp16 dispatch (csrc/conv_f16.hip), never its microbenchmark hooks.  A split-K

@@ -1,0 +1,46 @@
+"""Per-kernel HBM traffic from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in separate runs of the
+same serial workload, scripts/gpu_r3_prof.sh), keyed by kernel instantiation exactly as bench.py
+groups its per-op timings (yv7.runtime.kernel_key of the names yv7_op_kernels reports).
+
+gfx950 corrections (MI355X_MICROARCH.md, HBM section): read bytes = 2 x FETCH_SIZE (64 B counted per
+128-B request of a wide streaming read), WRITE_SIZE exact for 16-B stores; both reported in KiB.
+usage: python scripts/pmc_traffic_kernels.py FETCH_DIR WRITE_DIR OUT.json
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), 'yolo-series_amd'))
+from yv7.runtime import kernel_key  # noqa: E402
+
+
+def load(d, counter):
+    out = collections.defaultdict(list)
+    for f in glob.glob(f'{d}/**/*counter_collection.csv', recursive=True):
+        for r in csv.DictReader(open(f)):
+            if r['Counter_Name'] == counter:
+                out[kernel_key(r['Kernel_Name'])].append(float(r['Counter_Value']) * 1024.0)
+    return out
+
+
+def main(fdir, wdir, dst):
+    fetch, write = load(fdir, 'FETCH_SIZE'), load(wdir, 'WRITE_SIZE')
+    res = {'units': 'HBM bytes per launch: read = 2 x FETCH_SIZE, write = WRITE_SIZE (gfx950 corrections, '
+                    'MI355X_MICROARCH.md); separate --pmc passes of the same serial workload',
+           'kernels': {}}
+    for k, v in sorted(fetch.items(), key=lambda kv: -sum(kv[1])):
+        w = write.get(k, [])
+        n = len(v)
+        res['kernels'][k] = {'launches': n, 'read_bytes_per_launch': 2.0 * sum(v) / n,
+                             'write_bytes_per_launch': sum(w) / max(len(w), 1),
+                             'hbm_bytes_per_launch': 2.0 * sum(v) / n + sum(w) / max(len(w), 1)}
+    json.dump(res, open(dst, 'w'), indent=1)
+    for k, r in list(res['kernels'].items())[:12]:
+        print(f'{k[:80]:80s} n={r["launches"]:4d} {r["hbm_bytes_per_launch"] / 1e6:9.1f} MB')
+
+
+if __name__ == '__main__':
+    main(*sys.argv[1:4])

@@ -131,3 +131,90 @@ def test_bench_config_inflight_nms(batch):
         for b in range(B):
             n = int(cw[b])
             assert torch.equal(s[b, :n], sw[b, :n]) and torch.equal(d[b, :n], dw[b, :n]), (i, b)
+
+
+def test_w6_config_fp16_every_op():
+    """BASELINE configs[3]: yolov7-w6 (P6) 1280x1280 at batch 8 — the bench line's exact dispatch
+    (kernel choice depends on each layer's tile count: split-K in four on 512->512 @20, the persistent
+    rings on the 1280 / 640 / 320 stages, ReOrg fused into the input packing, the 4-level Detect
+    head).  Every op against a plain PyTorch fp32 reference on its own input (tests/opcheck.py), then
+    the whole network against the CPU oracle on images 0 and 7, layer by layer.
+    Reference: cfg/deploy/yolov7-w6.yaml; ReOrg models/common.py:48-53; Detect models/yolo.py:42-63."""
+    Bw, Hw = 8, 1280
+    xb = frames(Bw, Hw, Hw, seed=25)
+    m = fresh_model('yolov7-w6').to(DEV).half()
+    plan = m.plan()
+    x = xb.to(DEV).half()
+    N = plan.num_rows(Hw, Hw)
+    z1 = torch.empty((Bw, N, plan.no), dtype=torch.float32, device=DEV)
+    rb = torch.empty((Bw, N, 4), dtype=torch.float32, device=DEV)
+    plan.forward_into(x, z1, rowbest=rb)       # bench.py's call
+    z, xs = plan.forward(x)
+    torch.cuda.synchronize()
+    assert torch.equal(z, z1), 'raw-logit output changed z'
+    out = check_ops(plan, x, Bw, Hw, Hw, raw=xs, z=z)
+    print('\nyolov7-w6 1280 bs8 fp16: ' + kernel_summary(out))
+    from oracle import yolo_ref
+    net, fused = oracle_net('yolov7-w6')
+    pick = [0, 7]
+    xp = xb[pick]
+    (zr, _), outs = yolo_ref.forward(net, fused, xp, return_all=True)
+    (ze, _), outs16 = yolo_ref.forward(net, fused, xp, return_all=True, half_storage=True)
+    worst = (0.0, None)
+    for i in sorted(plan.graph.layer_tensor):
+        ref = outs[i]
+        if not isinstance(ref, torch.Tensor):
+            continue
+        got = plan.layer_output(i, Bw, Hw, Hw)[pick].cpu()
+        e = rms_rel(got, ref)
+        bar = max(5e-3, 1.5 * rms_rel(outs16[i], ref))
+        assert e <= bar, f'layer {i}: rms-rel {e:.3g} > {bar:.3g}'
+        worst = max(worst, (e, i))
+    print(f'oracle images {pick}: worst layer rms-rel {worst[0]:.3g} at layer {worst[1]}')
+    zc = z[pick].cpu()
+    sc = zr.abs().clamp(min=1)
+    print(f'z vs fp32 oracle: coord rel {((zc - zr).abs() / sc)[..., :4].max():.3g} '
+          f'(reference half() emulation {((ze - zr).abs() / sc)[..., :4].max():.3g})')
+
+
+def test_fp8_config_every_op(batch):
+    """BASELINE configs[4]: the product fp8 plan at yolov7 640 batch 32 (bench.py --dtype fp8).  The fp16
+    ops against plain PyTorch fp32 references (tests/opcheck.py), every fp8 op against the restatement of
+    its arithmetic applied to the very fp16 input it read (e4m3 input on the op's power-of-two scale, the
+    plan's per-channel e4m3 weights, fp32 accumulation, bias, activation; oracle.yolo_ref.fp8_e4m3 =
+    torch.float8_e4m3fn rounding), output within 2e-3 of max|y|."""
+    import torch.nn.functional as F
+
+    import plan_interp
+    from oracle import yolo_ref
+    from yv7 import _lib as L
+    from yv7.runtime import Plan
+    m = fresh_model('yolov7').to(DEV).half()
+    plan = Plan.fp8_from_model(m, DEV)
+    x = batch.to(DEV).half()
+    N = plan.num_rows(H, W)
+    z = torch.empty((B, N, plan.no), dtype=torch.float32, device=DEV)
+    rb = torch.empty((B, N, 4), dtype=torch.float32, device=DEV)
+    plan.forward_into(x, z, rowbest=rb)
+    z2, xs = plan.forward(x)
+    torch.cuda.synchronize()
+    assert torch.equal(z, z2)
+    out = check_ops(plan, x, B, H, W, raw=xs, z=z2, skip_fp8=True)
+    blob = plan.graph.weight_blob()
+    acts = {L.ACT_SILU: F.silu, L.ACT_LEAKY: lambda t: F.leaky_relu(t, 0.1), L.ACT_NONE: lambda t: t}
+    worst, n = 0.0, 0
+    for o in plan.graph.ops:
+        if o.get('wfmt', 0) != L.WFMT_FP8:
+            continue
+        xin = plan.tensor_view(o['src'], B, H, W)[..., o['src_coff']:o['src_coff'] + o['cin']].float()
+        xq = yolo_ref.fp8_e4m3(xin / o['xscale']) * o['xscale']
+        w = plan_interp._weights_f8(blob, o['w_off'], o['cout'], o['cin'], o['s_off']).reshape(o['cout'], -1).to(DEV)
+        b = plan_interp._bias(blob, o['b_off'], o['cout']).to(DEV)
+        want = acts[o['act']](xq.reshape(-1, o['cin']) @ w.t() + b)
+        got = plan.tensor_view(o['dst'], B, H, W)[..., o['dst_coff']:o['dst_coff'] + o['cout']].float()
+        err = ((got.reshape(-1, o['cout']) - want).abs().max() / want.abs().max().clamp(min=1e-3)).item()
+        assert err < 2e-3, f'fp8 op {o["cin"]}->{o["cout"]}: max-norm rel err {err:.3g}'
+        worst = max(worst, err)
+        n += 1
+    print(f'\nyolov7 640 bs32 fp8: {kernel_summary(out)} (fp16 ops); {n} fp8 ops, worst max-norm rel err {worst:.3g}')
+    assert n >= 10

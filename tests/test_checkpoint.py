@@ -56,3 +56,59 @@ def test_pickled_checkpoint_folds_match_oracle(tmp_path):
         w, b = head.head_weights(j)
         assert torch.equal(w, fused[head.i][j][0]) and torch.equal(b, fused[head.i][j][1])
     assert checked == 89   # yolov7: 82 Conv / RepConv layers + SPPCSPC's 7
+
+
+# Instance attribute trees the reference's constructors create (plain attributes, submodules,
+# parameters, buffers), read from the reference source: Conv models/common.py:101-105, SPPCSPC
+# common.py:264-274, ImplicitA / ImplicitM common.py:433-453, RepConv common.py:468-496 (training form;
+# rbr_identity is a BatchNorm2d when c1 == c2 and s == 1, else a plain None attribute), Detect
+# models/yolo.py:30-40, IDetect yolo.py:104-117 (+ `stride`, set on the head by Model.__init__,
+# yolo.py:545), MP / SP common.py:30-45, Concat common.py:56-59, nn.Upsample (torch's own).  Every
+# top-level layer also carries parse_model's i, f, type, np (yolo.py:806-808).
+REF_TREES = {
+    'Conv': (set(), {'conv', 'bn', 'act'}, set(), set()),
+    'SPPCSPC': (set(), {'cv1', 'cv2', 'cv3', 'cv4', 'cv5', 'cv6', 'cv7', 'm'}, set(), set()),
+    'ImplicitA': ({'channel', 'mean', 'std'}, set(), {'implicit'}, set()),
+    'ImplicitM': ({'channel', 'mean', 'std'}, set(), {'implicit'}, set()),
+    'RepConv': ({'deploy', 'groups', 'in_channels', 'out_channels'}, {'act', 'rbr_dense', 'rbr_1x1'}, set(), set()),
+    'Detect': ({'nc', 'no', 'nl', 'na', 'grid', 'stride'}, {'m'}, set(), {'anchors', 'anchor_grid'}),
+    'IDetect': ({'nc', 'no', 'nl', 'na', 'grid', 'stride'}, {'m', 'ia', 'im'}, set(), {'anchors', 'anchor_grid'}),
+    'MP': (set(), {'m'}, set(), set()),
+    'SP': (set(), {'m'}, set(), set()),
+    'Concat': ({'d'}, set(), set(), set()),
+}
+PARSE_ATTRS = {'i', 'f', 'type', 'np'}
+
+
+def _tree(mod):
+    plain = {k for k in vars(mod) if not k.startswith('_') and k != 'training'}
+    return plain, set(mod._modules), set(mod._parameters), set(mod._buffers)
+
+
+def test_module_attribute_trees_match_reference():
+    """Every module of the product's unfused Model (what a training checkpoint pickles, train.py:468-469)
+    has exactly the reference constructor's attribute tree: unpickling a reference checkpoint gives the
+    product's classes nothing less (a method of this package needing an attribute the reference does not
+    create would fail on load) and nothing more.  yolov7-train (IDetect, RepConv), yolov7 (Detect),
+    yolov7-tiny (MP / SP / LeakyReLU Convs)."""
+    from models.yolo import Model
+    seen = set()
+    for name in ('yolov7-train', 'yolov7', 'yolov7-tiny'):
+        m = Model(name)
+        top = {id(x) for x in m.model}
+        for mod in m.modules():
+            cls = type(mod).__name__
+            if cls not in REF_TREES and cls != 'Upsample':
+                continue
+            plain, subs, params, bufs = _tree(mod)
+            if id(mod) in top:
+                assert PARSE_ATTRS <= plain, (name, cls, PARSE_ATTRS - plain)
+                plain -= PARSE_ATTRS
+            if cls == 'Upsample':
+                continue
+            rp, rs, rpar, rb = (set(v) for v in REF_TREES[cls])
+            if cls == 'RepConv':   # rbr_identity: a BatchNorm2d (c1 == c2, s == 1) or a plain None
+                (rs if isinstance(mod.rbr_identity, torch.nn.BatchNorm2d) else rp).add('rbr_identity')
+            assert (plain, subs, params, bufs) == (rp, rs, rpar, rb), (name, cls, plain, subs, params, bufs)
+            seen.add(cls)
+    assert seen == set(REF_TREES), set(REF_TREES) - seen

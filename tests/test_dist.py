@@ -52,6 +52,75 @@ def _worker(rank, world, port, q):
         dist.destroy_process_group()
 
 
+class _HostPlan:
+    """Test double of yv7.runtime.Plan on the host: z row 0 of image b carries the image's global id
+    (the x value at [b, 0, 0, 0]), so the detections that come back identify the image they belong to."""
+    device = torch.device('cpu')
+    no = 6
+
+    def num_rows(self, H, W):
+        return 4
+
+    def forward_into(self, x, z, rowbest=None, stream=None, ws_slot=0):
+        z.zero_()
+        z[:, :, 0] = x[:, 0, 0, 0].view(-1, 1)
+
+
+def _host_nms(z, conf, iou, max_det, out, rowbest):
+    det, src, cnt = out
+    det.zero_()
+    det[:, :, 0] = z[:, 0, 0].view(-1, 1)
+    src.copy_(z[:, 0, 0].to(torch.int64).view(-1, 1).expand_as(src))
+    cnt.copy_(z[:, 0, 0].to(torch.int32))
+
+
+def _inflight_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, 'yolo-series_amd'), root]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from yv7.dist import gather_detections
+        from yv7.runtime import Inflight
+        B, S, nb = 3, 3, 7
+        run = Inflight(_HostPlan(), B, 2, 2, streams=S, max_det=5, post=gather_detections, nms=_host_nms)
+        got = {}
+        for h in range(nb):
+            x = torch.zeros(B, 3, 2, 2)
+            x[:, 0, 0, 0] = torch.arange(B) + h * B * world + rank * B     # global image ids of this rank's slice
+            assert run.submit(x) == h
+            if h >= S - 1:   # S batches in flight, collect the oldest
+                d, s_, c = run.result(h - S + 1)
+                got[h - S + 1] = c.tolist()
+        for j in range(nb - S + 1, nb):
+            got[j] = run.result(j)[2].tolist()
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_inflight_gather_order():
+    """yv7.runtime.Inflight (bench.py's serving schedule: S batches in flight, post= the per-batch
+    detection all-gather) across two ranks: every rank's result for batch h is batch h's detections of
+    the whole global batch, in global image order — submissions pair up across ranks in order, no slot
+    hands back another batch's buffers."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_inflight_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got in res:
+        assert sorted(got) == list(range(7))
+        for h, c in got.items():
+            assert c == list(range(h * 6, h * 6 + 6)), (rank, h, c)
+
+
 def test_shard_partition():
     for B, W in [(256, 8), (32, 1), (10, 4), (3, 4)]:
         parts = [shard(B, r, W) for r in range(W)]
@@ -93,6 +162,7 @@ def test_bench_launcher_starts_ranks():
     assert len(lines) == 1, out.stdout
     r = lines[0]
     assert r['n_gpus'] == 2 and r['world_size_seen'] == 2 and r['all_ranks_ok'] and r['global_batch'] == 6
+    assert r['per_rank_world_size_seen'] == [2, 2] and len(r['allgather_us_per_batch']) == 2
 
 
 @pytest.mark.gpu

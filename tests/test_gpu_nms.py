@@ -85,34 +85,68 @@ def test_nms_on_model_outputs_bitexact(name):
         _compare(zr, **kw)
 
 
-def test_end_to_end_detections_match():
-    """GPU forward + GPU NMS vs oracle forward + oracle NMS on the same frames (fp32 plan).
+@pytest.mark.parametrize('name', ['yolov7', 'yolov7-tiny'])
+def test_end_to_end_kept_rows_exact(name):
+    """GPU forward + GPU NMS vs oracle forward + oracle NMS on the same frames (fp32 plan): kept anchor
+    rows and class ids EQUAL (north_star: "kept-box indices bit-exact"), boxes / scores within the
+    z tolerance.
 
-    Same z in: GPU NMS == oracle NMS bit for bit (checked on the GPU's z).  Different z (fp32
-    summation order, see tests/parity.py): NMS decisions can flip only where a score or an IoU sits
-    within that noise of a threshold, so >= 99 % of the oracle's kept rows must be kept by the GPU,
-    with the same class."""
+    The two forwards sum in different orders (tests/parity.py), so an NMS decision whose operands sit
+    within float noise of its threshold may go either way; tests/margin.py removes exactly those
+    candidates (noise anchored on the float64 oracle, general.py:653,683-684,702-706) from BOTH z
+    tensors, and every remaining decision must then agree — the full kept list (max_det large, the
+    batched path) and detect.py's call (max_det 300, the one-launch nms_fast path)."""
+    from margin import noise_rows
     from oracle import nms_ref, yolo_ref
-    name = 'yolov7'
+    from utils.general import nms_batched, non_max_suppression
     x = frames(2, 640, 640, seed=7)
     net, fused = oracle_net(name)
     zr, _ = yolo_ref.forward(net, fused, x)
+    z64, _ = yolo_ref.forward64(net, fused, x)
     m = fresh_model(name).to(DEV)
-    z, _ = m(x.to(DEV))
-    from utils.general import non_max_suppression
-    out_g, rows_g = non_max_suppression(z, 0.25, 0.45, return_rows=True)
-    out_r, rows_r = nms_ref.non_max_suppression(zr, 0.25, 0.45, return_rows=True)
-    out_x, rows_x = nms_ref.non_max_suppression(z.cpu(), 0.25, 0.45, return_rows=True)
-    for i in range(2):
-        assert torch.equal(rows_g[i].cpu(), rows_x[i]) and torch.equal(out_g[i].cpu(), out_x[i])
-        rg, rr = rows_g[i].cpu().tolist(), rows_r[i].tolist()
-        common = set(rg) & set(rr)
-        print(f'\nimage {i}: oracle kept {len(rr)}, gpu kept {len(rg)}, common {len(common)}')
-        assert len(common) >= 0.99 * len(rr), (len(common), len(rr))
-        ig = {r: k for k, r in enumerate(rg)}
-        for k, r in enumerate(rr):
-            if r in ig:
-                assert out_g[i][ig[r]][5].item() == out_r[i][k][5].item()
+    zg, _ = m(x.to(DEV))
+    zg = zg.cpu()
+    conf, iou = 0.25, 0.45
+    zr2, zg2 = zr.clone(), zg.clone()
+    for b in range(2):
+        drop, st = noise_rows(zr[b], z64[b], zg[b], conf, iou)
+        zr2[b, drop, 4] = 0.0
+        zg2[b, drop, 4] = 0.0
+        print(f'\n{name} image {b}: {st}')
+        assert st['rows_dropped'] <= 0.01 * max(st['candidates'], 1) + 2, st
+    out_r, rows_r = nms_ref.non_max_suppression(zr2, conf, iou, return_rows=True, max_det=30000)
+    det, src, cnt = nms_batched(zg2.to(DEV), conf, iou, max_det=4096)
+    out_g300, rows_g300 = non_max_suppression(zg2.to(DEV), conf, iou, return_rows=True)
+    e64 = (zr2.double() - z64).abs() + (zg2.double() - z64).abs()
+    for b in range(2):
+        n = int(cnt[b])
+        rg, rr = src[b, :n].cpu(), rows_r[b]
+        assert n < 4096 and set(rg.tolist()) == set(rr.tolist()), f'image {b}: kept rows differ'
+        # order: descending score; only rows whose scores are within noise of each other may swap
+        if not torch.equal(rg, rr):
+            pos = {r: k for k, r in enumerate(rr.tolist())}
+            for k, r in enumerate(rg.tolist()):
+                j = pos[r]
+                lo, hi = min(j, k), max(j, k)
+                s = out_r[b][lo:hi + 1, 4].double()
+                assert (s.max() - s.min()).item() <= 1e-5, f'image {b}: row {r} at {k}, oracle {j}'
+        dg = det[b, :n].cpu()
+        og = {r: dg[k] for k, r in enumerate(rg.tolist())}
+        for k, r in enumerate(rr.tolist()):
+            g_, o_ = og[r], out_r[b][k]
+            assert g_[5] == o_[5], f'image {b}: row {r} class'
+            tol = 1e-4 * o_[:4].abs().clamp(min=1) + 2 * e64[b, r, :4].max().item() + 1e-4
+            assert ((g_[:4] - o_[:4]).abs() <= tol).all() and abs(g_[4] - o_[4]) <= 1e-4
+        # detect.py's call: max_det 300 = the first 300 of the full list (set; boundary ties allowed)
+        r300 = set(rows_g300[b].cpu().tolist())
+        want = rr[:300].tolist()
+        if len(rr) > 300:
+            tied = abs(float(out_r[b][299, 4]) - float(out_r[b][300, 4])) <= 1e-5
+        else:
+            tied = False
+        if not tied:
+            assert r300 == set(want), f'image {b}: max_det 300 rows differ'
+        print(f'{name} image {b}: oracle kept {len(rr)} (max_det 300: {len(r300)}), equal rows and classes')
 
 
 @pytest.mark.parametrize('kw', [dict(conf_thres=0.25, iou_thres=0.45, topk=100),

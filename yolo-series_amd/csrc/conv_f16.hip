@@ -1687,16 +1687,6 @@ hipError_t launch_p8_t(const ConvParams& p, int grid, hipStream_t st) {
     YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 20>), dim3(grid), dim3(512), 0, st, p);
     return hipGetLastError();
   }
-  if (p.act == 1 && p.variant >= 241 && p.variant <= 255) {   // experiments (SiLU layers only; 244 = 231)
-    switch (p.variant - 240) {
-      case 15: YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 0>), dim3(grid), dim3(512), 0, st, p); return hipGetLastError();
-#define P8X(o) case o: YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, o>), dim3(grid), dim3(512), 0, st, p); return hipGetLastError();
-      P8X(1) P8X(2) P8X(8) P8X(5) P8X(12) P8X(13)
-      case 4: break;   // the default
-#undef P8X
-      default: break;
-    }
-  }
   // XCD-major tile order (OPT 4): 1x1 1024->1024 @40 140 -> 133 us, 3x3 layers unchanged (tune_ops)
   if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 4>), dim3(grid), dim3(512), 0, st, p);
   else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 2, 4>), dim3(grid), dim3(512), 0, st, p);
@@ -2168,6 +2158,9 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (pcfg == 1) return launch_t<128, 128, 2, false, false, 1, true>(p, st);
     return launch_t<64, 128, 1, false, false, 1, true>(p, st);
   }
+  // the 3x3 halo ring (conv_hring.hip): 260 = 128-channel tiles, 261 = 256-channel tiles
+  if (!det && (variant == 260 || variant == 261) && hring_supported(p))
+    return launch_conv_hring(p, variant == 261 ? 256 : 128, device_cus(), st);
   if (!det && variant == 0 && p.cout > 32 && p.cout <= 1024 && p.cout % 8 == 0) {
     // Persistent ring (scripts/convbench.hip, bs 32, same box, us): short-K 1x1 layers and the
     // 128-channel / low-resolution 512-channel 3x3 layers, whose per-tile fill + epilogue the
@@ -2240,7 +2233,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 222) return one ? launch_pp<128, 128, 2, 2, true>(p, 2, st) : launch_pp<128, 128, 2, 2, false>(p, 2, st);
     if (variant == 223) return one ? launch_pp<256, 128, 4, 2, true>(p, 1, st) : launch_pp<256, 128, 4, 2, false>(p, 1, st);
     // 8-phase persistent ring (conv_f16_p8_kernel)
-    if ((variant == 231 || variant == 233 || variant == 237 || (variant > 240 && variant < 256)) && (one || p.cin % BKE == 0))
+    if ((variant == 231 || variant == 233 || variant == 237) && (one || p.cin % BKE == 0))
       return launch_p8(p, one, st);
     // weight-stationary 1x1 rings (conv_f16_pring_kernel, WS): 234 = 128 x 256 tiles (K <= 256),
     // 235 = 256 x 128 (K <= 256), 236 = 128 x 128 (K <= 512)

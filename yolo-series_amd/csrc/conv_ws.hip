@@ -51,8 +51,9 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint3
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, vo, so, 0, 0);
 }
 
-// SCHED (experiments, variants 17-19): 0 = the MFMA / ds_read / VALU issue pattern below, 1 = no
-// scheduling directives, 2 = MFMA / ds_read interleave only, 3 = pattern + s_setprio around the MFMAs
+// SCHED: 0 = the MFMA / ds_read / VALU issue pattern below (1 = no scheduling directives, 2 = MFMA /
+// ds_read interleave only, 3 = pattern + s_setprio around the MFMAs: round-2 experiments, all slower,
+// profiles/r2_ws64_sched_tune.txt; no longer launched)
 template <int ACT, int SCHED = 0>
 __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
@@ -289,12 +290,6 @@ hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st) {
   if (!ws64_supported(p)) return hipErrorInvalidValue;
   const int T = p.B * (p.H / TS) * (p.W / TS);
   const int grid = T < num_cus() ? T : num_cus();
-  if (p.act == 1 && p.variant >= 17 && p.variant <= 19) {   // scheduling experiments (SiLU layers)
-    if (p.variant == 17) YV7_LAUNCH((conv3x3_ws64_kernel<1, 1>), dim3(grid), dim3(NT), 0, st, p);
-    else if (p.variant == 18) YV7_LAUNCH((conv3x3_ws64_kernel<1, 2>), dim3(grid), dim3(NT), 0, st, p);
-    else YV7_LAUNCH((conv3x3_ws64_kernel<1, 3>), dim3(grid), dim3(NT), 0, st, p);
-    return hipGetLastError();
-  }
   if (p.act == 1) YV7_LAUNCH((conv3x3_ws64_kernel<1>), dim3(grid), dim3(NT), 0, st, p);
   else if (p.act == 2) YV7_LAUNCH((conv3x3_ws64_kernel<2>), dim3(grid), dim3(NT), 0, st, p);
   else YV7_LAUNCH((conv3x3_ws64_kernel<0>), dim3(grid), dim3(NT), 0, st, p);

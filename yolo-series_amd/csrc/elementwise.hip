@@ -123,14 +123,18 @@ __global__ __launch_bounds__(NT) void copy_kernel(const T* __restrict__ x, int B
 
 // ---- SPPCSPC pool cascade (common.py:271, 276-280 with k = (5, 9, 13)): the three stride-1 pools
 //      p5 = pool5(x), p9 = pool5(p5), p13 = pool5(p9) (max is associative; -inf padding keeps the
-//      cascade exact) in one launch.  Block = one image x 32 channels: the whole H x W x 32 plane
-//      is staged in LDS once and ping-pongs between two buffers, each pool reads LDS only; every
-//      stage's output also leaves as 16-byte stores into its concat slice.  Needs H*W <= 512 (fp16).
+//      cascade exact) in one launch.  Block = one image x 16 channels: the whole H x W x 16 plane is
+//      staged in LDS once; each 5 x 5 pool runs separably (a 5-wide row max into a scratch plane, then
+//      a 5-tall column max: 10 LDS reads per output instead of 25; taps outside the image re-read the
+//      centre, max being idempotent = the -inf padding), ping-ponging between two planes; every
+//      stage's output also leaves as 16-byte stores into its concat slice.
+constexpr int SPP_CG = 16;
+
 template <typename T>
 __global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x, int B, int H, int W, int xc,
                                                          int coff, int C, T* __restrict__ y) {
   constexpr int V = Vec<T>::N;
-  constexpr int CG = 32;                 // channels per block
+  constexpr int CG = SPP_CG;             // channels per block
   constexpr int NCH = CG / V;            // 16-byte chunks per pixel
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int groups = C / CG;
@@ -138,47 +142,47 @@ __global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x
   const int npx = H * W, items = npx * NCH;
   u4* buf0 = reinterpret_cast<u4*>(lds);
   u4* buf1 = buf0 + items;
+  u4* tmp = buf1 + items;
   for (int i = threadIdx.x; i < items; i += NT) {
     const int px = i / NCH, ch = i - px * NCH, h = px / W, w = px - h * W;
     buf0[i] = *reinterpret_cast<const u4*>(x + pix_index(b, h, w, H, W) * xc + coff + c0 + ch * V);
   }
   __syncthreads();
+  auto vmax = [](u4 a, u4 c) -> u4 {
+    if constexpr (sizeof(T) == 2) {   // packed fp16 max (v_pk_max_f16)
+      typedef _Float16 hv8 __attribute__((ext_vector_type(8)));
+      return __builtin_bit_cast(u4, __builtin_elementwise_max(__builtin_bit_cast(hv8, a), __builtin_bit_cast(hv8, c)));
+    } else {
+      typedef float fv4 __attribute__((ext_vector_type(4)));
+      return __builtin_bit_cast(u4, __builtin_elementwise_max(__builtin_bit_cast(fv4, a), __builtin_bit_cast(fv4, c)));
+    }
+  };
   u4* src = buf0;
   u4* dst = buf1;
   for (int stage = 1; stage <= 3; ++stage) {
-    for (int i = threadIdx.x; i < items; i += NT) {
-      const int px = i / NCH, ch = i - px * NCH, h = px / W, w = px - h * W;
-      // 25 independent LDS reads (taps outside the image re-read the centre: max is idempotent)
-      u4 tv[25];
+    for (int i = threadIdx.x; i < items; i += NT) {   // row max: 5 taps along w
+      const int px = i / NCH, ch = i - px * NCH, w = px % W;
+      u4 m = src[i];
 #pragma unroll
-      for (int dy = -2; dy <= 2; ++dy)
-#pragma unroll
-        for (int dx = -2; dx <= 2; ++dx) {
-          const int hi = h + dy, wi = w + dx;
-          const bool in = (unsigned)hi < (unsigned)H && (unsigned)wi < (unsigned)W;
-          tv[(dy + 2) * 5 + dx + 2] = src[(in ? hi * W + wi : px) * NCH + ch];
-        }
-      u4 o;
-      if constexpr (sizeof(T) == 2) {   // packed fp16 max (v_pk_max_f16), 8 channels per 4 ops
-        typedef _Float16 hv8 __attribute__((ext_vector_type(8)));
-        hv8 m = __builtin_bit_cast(hv8, tv[0]);
-#pragma unroll
-        for (int k = 1; k < 25; ++k) m = __builtin_elementwise_max(m, __builtin_bit_cast(hv8, tv[k]));
-        o = __builtin_bit_cast(u4, m);
-      } else {
-        T m[V];
-#pragma unroll
-        for (int e = 0; e < V; ++e) m[e] = neg_inf<T>();
-#pragma unroll
-        for (int k = 0; k < 25; ++k) {
-          const T* e = reinterpret_cast<const T*>(&tv[k]);
-#pragma unroll
-          for (int q = 0; q < V; ++q) m[q] = tmax(m[q], e[q]);
-        }
-        o = *reinterpret_cast<const u4*>(m);
+      for (int dx = -2; dx <= 2; ++dx) {
+        if (dx == 0) continue;
+        const bool in = (unsigned)(w + dx) < (unsigned)W;
+        m = vmax(m, src[(in ? px + dx : px) * NCH + ch]);
       }
-      dst[i] = o;
-      *reinterpret_cast<u4*>(y + pix_index(b, h, w, H, W) * xc + coff + stage * C + c0 + ch * V) = o;
+      tmp[i] = m;
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < items; i += NT) {   // column max: 5 taps along h
+      const int px = i / NCH, ch = i - px * NCH, h = px / W, w = px - h * W;
+      u4 m = tmp[i];
+#pragma unroll
+      for (int dy = -2; dy <= 2; ++dy) {
+        if (dy == 0) continue;
+        const bool in = (unsigned)(h + dy) < (unsigned)H;
+        m = vmax(m, tmp[(in ? px + dy * W : px) * NCH + ch]);
+      }
+      dst[i] = m;
+      *reinterpret_cast<u4*>(y + pix_index(b, h, w, H, W) * xc + coff + stage * C + c0 + ch * V) = m;
     }
     __syncthreads();
     u4* t = src;
@@ -288,15 +292,15 @@ hipError_t launch_copy(int dtype, const void* x, int B, int H, int W, int xc, in
 
 bool spp_cascade_supported(int dtype, int H, int W, int C) {
   const int V = dtype == 1 ? 8 : 4;
-  return C % 32 == 0 && (size_t)2 * H * W * (32 / V) * 16 <= 64 * 1024;
+  return C % SPP_CG == 0 && (size_t)3 * H * W * (SPP_CG / V) * 16 <= 64 * 1024;
 }
 
 // x: the concat tensor (pitch xc) holding the pool input at channel slice [coff, coff + C); the three
 // pools go to [coff + C, coff + 2C), [coff + 2C, coff + 3C), [coff + 3C, coff + 4C) of the same tensor.
 hipError_t launch_spp_cascade(int dtype, void* x, int B, int H, int W, int xc, int coff, int C, hipStream_t st) {
   const int V = dtype == 1 ? 8 : 4;
-  const size_t lds = (size_t)2 * H * W * (32 / V) * 16;
-  const dim3 grid(B * (C / 32));
+  const size_t lds = (size_t)3 * H * W * (SPP_CG / V) * 16;
+  const dim3 grid(B * (C / SPP_CG));
   if (dtype == 1)
     YV7_LAUNCH(spp_cascade_kernel<_Float16>, grid, dim3(NT), lds, st, (const _Float16*)x, B, H, W, xc, coff, C,
                        (_Float16*)x);

@@ -625,8 +625,10 @@ __global__ __launch_bounds__(SORT_T) void nms_fast(const FastArgs a) {
       if (c) {
         const int k = base + __popcll(m & ((lane == 0) ? 0ull : (~0ull >> (64 - lane))));
         const uint64_t key = ((uint64_t)(~__float_as_uint(rr[u].conf)) << 32) | (uint32_t)row;
+        // the first FAST_LDS_KEYS keys go to LDS only; the global list is written past them and
+        // completed from LDS below only when the list outgrows the LDS sort
         if (k < FAST_LDS_KEYS) skeys[k] = key;
-        gkeys[k] = key;   // (the global copy is read only when the list outgrows the LDS sort)
+        else gkeys[k] = key;
       }
     }
   }
@@ -639,6 +641,7 @@ __global__ __launch_bounds__(SORT_T) void nms_fast(const FastArgs a) {
   else if (n <= 4 * SORT_T) sort_lds<4>(skeys, n, tid);
   else if (n <= FAST_LDS_KEYS) sort_lds<8>(skeys, n, tid);
   else {   // global bitonic over the whole list
+    for (int i = tid; i < FAST_LDS_KEYS; i += SORT_T) gkeys[i] = skeys[i];
     int P = 1;
     while (P < n) P <<= 1;
     for (int i = n + tid; i < P; i += SORT_T) gkeys[i] = ~0ull;

@@ -5,6 +5,7 @@
 // as a flat list of ops over NHWC tensors.  yv7_forward walks that list once per batch, launching
 // one kernel per op on the caller's stream (forward_once's per-layer loop, models/yolo.py:603-627,
 // without the Python dispatch); no allocation, no host sync, so callers can capture it in a graph.
+#include <cxxabi.h>
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -359,9 +360,9 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   const int kind = o.kind;
   if (is_f8(o)) return v == 81 || v == 82;   // fp8 1x1: staged quantize pass / fused quantization
   if (kind == YV7_OP_DETECT) return v == 92 || v == 97;
-  if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15 || (v >= 17 && v <= 19)) return true;
+  if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
-  return (v >= 201 && v <= 206) || (v >= 211 && v <= 218) || (v >= 221 && v <= 223) || (v >= 231 && v <= 238) || (v > 240 && v < 256);
+  return (v >= 201 && v <= 206) || (v >= 211 && v <= 218) || (v >= 221 && v <= 223) || (v >= 231 && v <= 238) || v == 260 || v == 261;
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {
@@ -400,8 +401,12 @@ int yv7_tensor_info(const yv7_plan* p, int id, int B, int H, int W, int64_t* off
   return 0;
 }
 
-int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, float* z, float* raw,
-                yv7_row_best* rowbest, void* ws, size_t ws_bytes, void* stream) {
+// The forward's op loop.  dry: launch nothing (yv7_kernels.h LaunchRec), record per op the host stubs
+// of the kernels the dispatch picks into *kernels (yv7_op_kernels); no workspace clearing, no events.
+static int forward_impl(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, float* z, float* raw,
+                        yv7_row_best* rowbest, void* ws, size_t ws_bytes, void* stream,
+                        std::vector<std::vector<const void*>>* kernels) {
+  const bool dry = kernels != nullptr;
   if (!p || !x || !z || !ws) return fail(YV7_E_ARG, "yv7_forward: null argument");
   if (x_dtype != YV7_DT_F32 && x_dtype != YV7_DT_F16) return fail(YV7_E_ARG, "yv7_forward: bad x_dtype");
   if (int rc = check_hw(p, B, H, W)) return rc;
@@ -409,8 +414,8 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   const auto off = tensor_offsets(p, B, H, W, &total);
   const SplitScratch scr = split_scratch(p, B, H, W, total);
   total = scr.end;
-  if (ws_bytes < total) return fail(YV7_E_WORKSPACE, "yv7_forward: workspace too small (need " +
-                                                         std::to_string(total) + " bytes)");
+  if (!dry && ws_bytes < total) return fail(YV7_E_WORKSPACE, "yv7_forward: workspace too small (need " +
+                                                                 std::to_string(total) + " bytes)");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   unsigned char* wsb = reinterpret_cast<unsigned char*>(ws);
   const unsigned char* wb = reinterpret_cast<const unsigned char*>(p->weights);
@@ -419,7 +424,7 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   // a workspace is cleared the first time it is seen with this layout (pointer, size AND the batch
   // geometry: (B, H, W) and (B, W, H) have equal sizes but different frames) and never again, until
   // the caller hands the memory back with yv7_workspace_forget (include/yv7.h).
-  {
+  if (!dry) {
     bool ready = false;
     for (const auto& w : p->ws_ready)
       if (w.ptr == ws && w.bytes == total && w.B == B && w.H == H && w.W == W) ready = true;
@@ -461,19 +466,26 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   // last op
   const bool rowbest_fused = rowbest && yv7::det_writes_rowbest(p->dtype);
   hipEvent_t* ev = nullptr;
-  if (p->prof_used < p->prof_max) {
-    ev = &p->events[(size_t)p->prof_used * 2 * p->ops.size()];
-    p->prof_used++;
-  }
+  // the forward's event slot is claimed only once every op has launched (below): a forward that fails
+  // part-way leaves the slot to the next one instead of a pair that was never recorded
+  if (!dry && p->prof_used < p->prof_max) ev = &p->events[(size_t)p->prof_used * 2 * p->ops.size()];
   // the op's (start, stop) pair rides on its kernel launches (yv7_kernels.h YV7_LAUNCH); cleared on
   // every way out of this function
   struct EventScope {
-    ~EventScope() { yv7::op_events() = yv7::OpEvents{}; }
+    ~EventScope() {
+      yv7::op_events() = yv7::OpEvents{};
+      yv7::launch_rec() = yv7::LaunchRec{};
+    }
   } event_scope;
+  if (dry) kernels->assign(p->ops.size(), {});
   size_t fused_until = 0;   // ops [.., fused_until) were launched as part of a fused group
   for (size_t i = 0; i < p->ops.size(); ++i) {
     const auto& o = p->ops[i];
     if (ev) yv7::op_events() = yv7::OpEvents{ev[2 * i], ev[2 * i + 1], 0};
+    if (dry) {
+      yv7::launch_rec() = yv7::LaunchRec{};
+      yv7::launch_rec().dry = true;
+    }
     switch (o.kind) {
       case YV7_OP_INPUT: {
         const auto& t = p->tensors[o.dst];
@@ -629,15 +641,53 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
         return fail(YV7_E_ARG, "yv7_forward: unknown op kind");
     }
     if (e != hipSuccess) return hip_fail(e, "yv7_forward launch");
+    if (dry) {
+      const auto& r = yv7::launch_rec();
+      for (int k = 0; k < r.n && k < 4; ++k) (*kernels)[i].push_back(r.fn[k]);
+    }
     if (ev && yv7::op_events().launches == 0) {   // no kernel of its own (a later op of a fused cascade)
       if ((e = hipEventRecord(ev[2 * i], st)) != hipSuccess || (e = hipEventRecord(ev[2 * i + 1], st)) != hipSuccess)
         return hip_fail(e, "hipEventRecord");
     }
   }
   yv7::op_events() = yv7::OpEvents{};
+  if (dry) return 0;
+  if (ev) p->prof_used++;
   if (rowbest && !rowbest_fused &&
       (e = yv7::launch_row_best(z, B, nrows, p->no, rowbest, st)) != hipSuccess)
     return hip_fail(e, "yv7_forward row scores");
+  return 0;
+}
+
+int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, float* z, float* raw,
+                yv7_row_best* rowbest, void* ws, size_t ws_bytes, void* stream) {
+  return forward_impl(p, x, x_dtype, B, H, W, z, raw, rowbest, ws, ws_bytes, stream, nullptr);
+}
+
+int yv7_op_kernels(yv7_plan* p, int B, int H, int W, char* buf, size_t bytes) {
+  if (!p || !buf || bytes == 0) return fail(YV7_E_ARG, "yv7_op_kernels: null argument");
+  std::vector<std::vector<const void*>> ks;
+  // dry run: the op loop with placeholder pointers (nothing is launched or dereferenced on the host)
+  static const float dummy[4] = {0, 0, 0, 0};
+  void* ph = const_cast<float*>(dummy);
+  if (int rc = forward_impl(p, ph, YV7_DT_F16, B, H, W, static_cast<float*>(ph), nullptr, nullptr, ph, 0, nullptr, &ks))
+    return rc;
+  std::string out;
+  for (size_t i = 0; i < ks.size(); ++i) {
+    out += std::to_string(i);
+    for (size_t k = 0; k < ks[i].size(); ++k) {
+      const char* mangled = hipKernelNameRefByPtr(ks[i][k], nullptr);
+      std::string name = mangled ? mangled : "?";
+      int st = 0;
+      char* dem = mangled ? abi::__cxa_demangle(mangled, nullptr, nullptr, &st) : nullptr;
+      if (dem && st == 0) name = dem;
+      std::free(dem);
+      out += (k ? "|" : "\t") + name;
+    }
+    out += "\n";
+  }
+  if (out.size() + 1 > bytes) return fail(YV7_E_ARG, "yv7_op_kernels: buffer too small (need " + std::to_string(out.size() + 1) + ")");
+  std::memcpy(buf, out.c_str(), out.size() + 1);
   return 0;
 }
 

@@ -22,8 +22,25 @@ inline OpEvents& op_events() {
   static thread_local OpEvents e;
   return e;
 }
+// Dry run (yv7_op_kernels): while `dry` is set, YV7_LAUNCH launches nothing and records the host stub
+// of the kernel the dispatch picked (runtime.cpp turns it into the symbol rocprofv3 reports).
+struct LaunchRec {
+  bool dry = false;
+  int n = 0;
+  const void* fn[4] = {nullptr, nullptr, nullptr, nullptr};
+};
+inline LaunchRec& launch_rec() {
+  static thread_local LaunchRec r;
+  return r;
+}
 #define YV7_LAUNCH(kernel, grid, block, shmem, st, ...)                                                    \
   do {                                                                                                     \
+    ::yv7::LaunchRec& lr_ = ::yv7::launch_rec();                                                           \
+    if (lr_.dry) {                                                                                         \
+      if (lr_.n < 4) lr_.fn[lr_.n] = reinterpret_cast<const void*>(kernel);                               \
+      lr_.n++;                                                                                             \
+      break;                                                                                               \
+    }                                                                                                      \
     ::yv7::OpEvents& ev_ = ::yv7::op_events();                                                             \
     hipExtLaunchKernelGGL(kernel, grid, block, shmem, st, ev_.launches ? nullptr : ev_.start, ev_.stop, 0, \
                           __VA_ARGS__);                                                                    \
@@ -168,6 +185,8 @@ bool halo_supported(const ConvParams& p);
 bool ws64_supported(const ConvParams& p);
 hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st);
 hipError_t launch_conv_halo(const ConvParams& p, hipStream_t st);
+bool hring_supported(const ConvParams& p);
+hipError_t launch_conv_hring(const ConvParams& p, int bn, int cus, hipStream_t st);
 hipError_t launch_input(int dtype, const void* x, int x_dtype, void* y, int B, int H, int W, int yc,
                         bool reorg, hipStream_t st);
 hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int Ho,

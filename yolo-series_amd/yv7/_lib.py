@@ -60,6 +60,7 @@ SIGNATURES = {
     'yv7_set_op_variant': (_i, [_vp, _i, _i]),
     'yv7_num_rows': (_i64, [_vp, _i, _i]),
     'yv7_forward': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
+    'yv7_op_kernels': (_i, [_vp, _i, _i, _i, ctypes.c_char_p, _sz]),
     'yv7_profile_enable': (_i, [_vp, _i]),
     'yv7_profile_read': (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_float)]),
     'yv7_tensor_info': (_i, [_vp, _i, _i, _i, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),

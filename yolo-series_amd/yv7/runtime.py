@@ -42,6 +42,45 @@ class _RowScores:
 row_scores = _RowScores()
 
 
+def _demangle(sym: str) -> str:
+    """Itanium C++ demangling through libstdc++'s __cxa_demangle (rocprofv3 reports some names mangled)."""
+    try:
+        cxx = ctypes.CDLL('libstdc++.so.6')
+        f = cxx.__cxa_demangle
+        f.restype = ctypes.c_void_p
+        st = ctypes.c_int()
+        p = f(sym.encode(), None, None, ctypes.byref(st))
+        if st.value != 0 or not p:
+            return sym
+        out = ctypes.string_at(p).decode()
+        ctypes.CDLL(None).free(ctypes.c_void_p(p))
+        return out
+    except (OSError, AttributeError):
+        return sym
+
+
+def kernel_key(name: str) -> str:
+    """A kernel instantiation's short key, the same for the names yv7_op_kernels reports and the
+    Kernel_Name column of a rocprofv3 trace: 'void yv7::(anonymous namespace)::k<1, 2>(yv7::ConvParams)'
+    -> 'k<1, 2>'."""
+    n = name.strip()
+    if n.startswith('_Z'):
+        n = _demangle(n)
+    if n.startswith('void '):
+        n = n[5:]
+    for pre in ('yv7::(anonymous namespace)::', 'yv7::'):
+        n = n.replace(pre, '')
+    depth = 0
+    for i, ch in enumerate(n):   # drop the parameter list: the first '(' outside template brackets
+        if ch == '<':
+            depth += 1
+        elif ch == '>':
+            depth -= 1
+        elif ch == '(' and depth == 0:
+            return n[:i]
+    return n
+
+
 class Plan:
     def __init__(self, graph, device, weights: torch.Tensor):
         self.graph = graph
@@ -196,6 +235,19 @@ class Plan:
         L.check(L.lib().yv7_profile_read(self._h, ctypes.byref(n), ms), 'yv7_profile_read')
         return n.value, list(ms)
 
+    def op_kernels(self, B, H, W):
+        """Per op, the kernel names (rocprofv3's demangled symbols) the dispatch launches for a
+        [B,3,H,W] forward (yv7_op_kernels: a dry run, nothing executes); [] for an op without a
+        kernel of its own (the later pools of the SPPCSPC cascade)."""
+        buf = ctypes.create_string_buffer(1 << 20)
+        with torch.cuda.device(self.device):
+            L.check(L.lib().yv7_op_kernels(self._h, B, H, W, buf, len(buf)), 'yv7_op_kernels')
+        out = [[] for _ in self.graph.ops]
+        for line in buf.value.decode().splitlines():
+            i, _, names = line.partition('\t')
+            out[int(i)] = names.split('|') if names else []
+        return out
+
     def op_costs(self, B, H, W, x_bytes=4, with_raw=True):
         """Per op: (kind, algorithmic FLOPs, algorithmic HBM bytes) for a [B,3,H,W] batch.
 
@@ -313,43 +365,55 @@ class Inflight:
     """
 
     def __init__(self, plan, B, H, W, streams=3, conf_thres=0.25, iou_thres=0.45, max_det=300, post=None,
-                 priorities=None):
+                 priorities=None, nms=None):
+        """nms(z, conf, iou, max_det, out, rowbest): the batched NMS (default utils.general.nms_batched).
+        A plan on a CPU device (test doubles: the multi-rank ordering tests on gloo) runs every
+        submission synchronously on the host — same slots, buffers and post() order, no streams."""
         self.plan, self.S = plan, max(1, int(streams))
         self.conf, self.iou, self.max_det, self.post = conf_thres, iou_thres, max_det, post
+        if nms is None:
+            from utils.general import nms_batched
+
+            def nms(z, conf, iou, max_det, out, rowbest):
+                return nms_batched(z, conf, iou, max_det=max_det, out=out, rowbest=rowbest)
+        self.nms = nms
         dev = plan.device
+        self.host = dev.type == 'cpu'
         N = plan.num_rows(H, W)
         if N <= 0:
             L.check(-2, f'yv7_num_rows(H={H}, W={W})')
         self.shape = (B, 3, H, W)
         S = self.S
         prios = list(priorities) if priorities is not None else [0] * S   # HIP stream priorities (-1 = high)
-        self.streams = [torch.cuda.Stream(dev, priority=prios[i % len(prios)]) for i in range(S)]
+        self.streams = [None if self.host else torch.cuda.Stream(dev, priority=prios[i % len(prios)]) for i in range(S)]
         self.z = [torch.empty((B, N, plan.no), dtype=torch.float32, device=dev) for _ in range(S)]
         self.rowbest = [torch.empty((B, N, 4), dtype=torch.float32, device=dev) for _ in range(S)]
         self.det = [torch.empty((B, max_det, 6), dtype=torch.float32, device=dev) for _ in range(S)]
         self.src = [torch.empty((B, max_det), dtype=torch.int64, device=dev) for _ in range(S)]
         self.cnt = [torch.empty((B,), dtype=torch.int32, device=dev) for _ in range(S)]
-        self.done = [torch.cuda.Event() for _ in range(S)]
+        self.done = [None if self.host else torch.cuda.Event() for _ in range(S)]
         self.out = [None] * S   # post()'s result per slot
         self.n = 0
 
     def submit(self, x):
         """Queue one batch; returns its handle (the submission index)."""
-        from utils.general import nms_batched
+        import contextlib
         if tuple(x.shape) != self.shape:
             raise ValueError(f'Inflight built for {self.shape}, got {tuple(x.shape)}')
         k = self.n % self.S
         s = self.streams[k]
-        s.wait_stream(torch.cuda.current_stream(self.plan.device))   # x is ready
+        if s is not None:
+            s.wait_stream(torch.cuda.current_stream(self.plan.device))   # x is ready
         self.plan.forward_into(x, self.z[k], rowbest=self.rowbest[k], stream=s, ws_slot=k)
-        with torch.cuda.stream(s):
-            nms_batched(self.z[k], self.conf, self.iou, max_det=self.max_det,
-                        out=(self.det[k], self.src[k], self.cnt[k]), rowbest=self.rowbest[k])
+        with (torch.cuda.stream(s) if s is not None else contextlib.nullcontext()):
+            self.nms(self.z[k], self.conf, self.iou, self.max_det, (self.det[k], self.src[k], self.cnt[k]),
+                     self.rowbest[k])
             out = (self.det[k], self.src[k], self.cnt[k])
             if self.post is not None:
                 out = self.post(*out)
         self.out[k] = out
-        self.done[k].record(s)
+        if self.done[k] is not None:
+            self.done[k].record(s)
         self.n += 1
         return self.n - 1
 
@@ -359,13 +423,15 @@ class Inflight:
         if not (self.n - self.S <= h < self.n):
             raise IndexError(f'batch {h} is no longer buffered (last {self.S} of {self.n} submissions)')
         k = h % self.S
-        self.done[k].synchronize()
+        if self.done[k] is not None:
+            self.done[k].synchronize()
         return self.out[k]
 
     def close(self):
         """Wait for every batch in flight (their buffers and workspaces are then free to go)."""
         for s in self.streams:
-            s.synchronize()
+            if s is not None:
+                s.synchronize()
 
     def __del__(self):
         try:
