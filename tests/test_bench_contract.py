@@ -28,6 +28,16 @@ def test_bench_json_line():
     # value is whole-job images/s over the timed steps
     assert abs(d['value'] - 32 * 1000.0 / d['ms_per_step']) / d['value'] < 0.02
     rf = d['roofline']
-    assert rf['bound'] == 'hbm' and rf['unit'] == 'GB/s' and rf['peak'] == 8000.0
+    assert (rf['bound'], rf['unit'], rf['peak']) in (('hbm', 'GB/s', 8000.0), ('mfma', 'TFLOP/s', 2500.0))
     assert 0.0 < rf['frac'] < 1.0 and abs(rf['frac'] - rf['achieved'] / rf['peak']) < 1e-3
+    # the dominant kernel is the first of the per-kernel table, and every row's frac = roof / time
+    top = rf['kernels_top5']
+    assert top[0]['kernel'] == rf['kernel'] and abs(top[0]['us_per_launch'] - rf['mean_launch_us']) < 1e-6
+    for r_ in top:
+        assert abs(r_['frac'] - r_['roof_us'] / r_['us_per_launch']) < 1e-3 and r_['bound'] in ('hbm', 'mfma')
+    assert all(top[i]['us_per_launch'] * top[i]['launches_per_forward'] >=
+               top[i + 1]['us_per_launch'] * top[i + 1]['launches_per_forward'] - 1e-6 for i in range(len(top) - 1))
     assert d['detail']['streams'] == 3 and d['detail']['mean_dets_per_image'] > 0
+    assert d['config']['resident_input_batches'] >= 4 and isinstance(d['config']['dispatch_env'], dict)
+    load = d['detail']['nms_load']
+    assert load['conf_0.25']['candidates_per_image'] >= load['conf_0.5']['candidates_per_image'] > 0

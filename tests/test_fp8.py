@@ -173,9 +173,12 @@ def test_gpu_fp8_map_parity(name):
     emu32, _ = metrics_ref.map_from_lists([d for d in nms_ref.non_max_suppression(ze, 0.25, 0.45)], gt)
     print(f'\n{name} fp8: mAP@0.5 vs fp32 oracle {m32:.4f} (oracle fp8 restatement vs fp32: {emu32:.4f}), '
           f'vs fp8 restatement {memu:.4f}; dets {[len(d) for d in pred]}')
-    # e4m3 costs this random-weight network most of its detections (the restatement loses as much as the
-    # kernels do); the GPU plan must be no worse than the restatement of its own arithmetic
+    # e4m3 costs this random-weight network a large share of its detections (the restatement loses as
+    # much as the kernels do): the GPU plan must be no worse than the restatement of its own arithmetic,
+    # and the config's measured cost is pinned by an absolute floor (MI355X, round 3: yolov7 0.588,
+    # yolov7-tiny 0.668 against the fp32 oracle; fp16 plans: >= 0.98)
     assert m32 >= emu32 - 0.02
+    assert m32 >= {'yolov7': 0.5, 'yolov7-tiny': 0.55}[name]
 
 
 @pytest.mark.gpu

@@ -2159,8 +2159,17 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     return launch_t<64, 128, 1, false, false, 1, true>(p, st);
   }
   // the 3x3 halo ring (conv_hring.hip): 260 = 128-channel tiles, 261 = 256-channel tiles
-  if (!det && (variant == 260 || variant == 261) && hring_supported(p))
-    return launch_conv_hring(p, variant == 261 ? 256 : 128, device_cus(), st);
+  if (!det && (variant == 260 || variant == 261 || variant == 262 || (variant >= 911 && variant <= 914)) &&
+      hring_supported(p))
+    return launch_conv_hring(p, variant == 261 ? 256 : variant == 260 ? 128 : 2, device_cus(), st);
+  // 3x3 stride-1 layers with 128-channel output tiles and at least one round of 16 x 16 x 128 tiles: the
+  // column-group halo ring (conv_hring.hip, variant 262).  Single-layer sweep, bs 32 640, same box
+  // (profiles/r3_hring2_tune.txt, us, dispatch -> 262): 3x3 128->128 @80 80.0 / 80.4 / 82.7 / 81.0 ->
+  // 67.2 / 67.9 / 69.3 / 68.4, 128->256 @80 139.1 -> 121.4.  YV7_HRING=0: off.
+  static const int hring = [] { const char* e = getenv("YV7_HRING"); return e ? atoi(e) : 1; }();
+  if (!det && variant == 0 && hring && hring_supported(p) && p.cout % 128 == 0 &&
+      (long)p.B * (p.Ho / 16) * (p.Wo / 16) * (p.cout / 128) >= device_cus())
+    return launch_conv_hring(p, 2, device_cus(), st);
   if (!det && variant == 0 && p.cout > 32 && p.cout <= 1024 && p.cout % 8 == 0) {
     // Persistent ring (scripts/convbench.hip, bs 32, same box, us): short-K 1x1 layers and the
     // 128-channel / low-resolution 512-channel 3x3 layers, whose per-tile fill + epilogue the
