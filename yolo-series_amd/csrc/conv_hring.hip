@@ -67,6 +67,14 @@ constexpr int wait_count(int i, int R, int PWN) {
   return n;
 }
 
+// The counted waits assume each wave's vector-memory ops issue exactly as written: every dummy DMA
+// present (identical dummies to one LDS address were merged by dead-store elimination — one op
+// instead of three in a block's last phases, so a wait retired one stage too few) and in program
+// order (weights, patch piece, epilogue stores).  Dummies of one phase therefore get distinct LDS
+// slots, and this compiler fence (no instruction) keeps the groups from being scheduled across
+// each other.
+__device__ __forceinline__ void dma_fence() { asm volatile("" ::: "memory"); }
+
 template <int N>
 __device__ __forceinline__ void vmwait() {
   static_assert(N >= 0 && N < 64, "vmcnt range");
@@ -83,8 +91,8 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring_kernel(const ConvParams 
   constexpr int NST = TM * TN / 2;          // epilogue stores per lane per tile
   constexpr int RING = 2 * PBUF;
   constexpr int BIAS = RING + R * STG;
-  constexpr int DUMMY = BIAS + 4096;
-  constexpr int LDS = DUMMY + 1024;
+  constexpr int DUMMY = BIAS + 4096;         // PWN + 1 KiB: one distinct slot per dummy of a phase
+  constexpr int LDS = DUMMY + (PWN + 1) * 1024;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   static_assert(TN % 2 == 0 && PWN >= 1, "tile shape");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
@@ -141,8 +149,9 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring_kernel(const ConvParams 
       for (int j = 0; j < PWN; ++j) dma16(wr, d + (wave + 8 * j) * 1024, wvo[j], so);
     } else {   // past the block's last tile: same op count, nothing fetched
 #pragma unroll
-      for (int j = 0; j < PWN; ++j) dma16(wr, smem + DUMMY, OOB, 0u);
+      for (int j = 0; j < PWN; ++j) dma16(wr, smem + DUMMY + j * 1024, OOB, 0u);
     }
+    dma_fence();
     if (++w_slot == R) w_slot = 0;
     if (++w_t == 9) {
       w_t = 0;
@@ -170,7 +179,8 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring_kernel(const ConvParams 
   p_offsets(0);
   auto issue_p = [&](int j) __attribute__((always_inline)) {
     if (p_it < ntl) dma16(xr, smem + (p_gc & 1) * PBUF + (wave + 8 * j) * 1024, pvo[j], (uint32_t)p_c * CK * 2);
-    else dma16(xr, smem + DUMMY, OOB, 0u);
+    else dma16(xr, smem + DUMMY + PWN * 1024, OOB, 0u);
+    dma_fence();
     if (j == PPW - 1) {
       ++p_gc;
       if (++p_c == nch) {
@@ -331,8 +341,8 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring2_kernel(const ConvParams
   constexpr int PB2 = 21 * 1024;            // one patch buffer (336 rows)
   constexpr int RING = 3 * PB2;
   constexpr int BIAS = RING + NSLOT * STG;
-  constexpr int DUMMY = BIAS + 4096;
-  constexpr int LDS = DUMMY + 1024;
+  constexpr int DUMMY = BIAS + 4096;        // 4 KiB: a distinct slot for each of a phase's 4 DMA ops
+  constexpr int LDS = DUMMY + 4 * 1024;
   static_assert(LDS <= 160 * 1024, "LDS budget");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
   float* bias_l = reinterpret_cast<float*>(smem + BIAS);
@@ -384,8 +394,9 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring2_kernel(const ConvParams
         dma16(wr, smem + RING + (slot0 + r) * STG + wave * 1024, wvo, (uint32_t)(((r * 3 + w_s) * p.cin + w_c * CK) * 2));
     } else {
 #pragma unroll
-      for (int r = 0; r < 3; ++r) dma16(wr, smem + DUMMY, OOB, 0u);
+      for (int r = 0; r < 3; ++r) dma16(wr, smem + DUMMY + r * 1024, OOB, 0u);
     }
+    dma_fence();
     ++w_ph;
     if (++w_s == 3) {
       w_s = 0;
@@ -417,8 +428,9 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring2_kernel(const ConvParams
     constexpr int J = decltype(jc)::value;
     const int gc = p_k / 3;
     const bool live = p_it < ntl && wave + 8 * J < 21;
-    const int dst = live ? (gc % 3) * PB2 + (wave + 8 * J) * 1024 : DUMMY;
+    const int dst = live ? (gc % 3) * PB2 + (wave + 8 * J) * 1024 : DUMMY + 3 * 1024;
     dma16(xr, smem + dst, live ? pvo[J] : OOB, live ? (uint32_t)p_c * CK * 2 : 0u);
+    dma_fence();
     if (++p_k % 3 == 0 && p_it < ntl) {
       if (++p_c == nch) {
         p_c = 0;
