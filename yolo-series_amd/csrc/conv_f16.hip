@@ -169,7 +169,7 @@ __device__ __forceinline__ DetTab det_tab_ptrs(unsigned char* smem) {
 }
 
 // Step 0 (every thread; the caller then syncs): the per-pixel table.
-template <int BM, int BN, int NTH>
+template <int BM, int BN, int NTH, bool ANC = true>
 __device__ __forceinline__ void det_table(const ConvParams& p, unsigned char* smem, int m0, int tid) {
   const DetTab t = det_tab_ptrs<BM, BN>(smem);
   const int hw = p.Ho * p.Wo;
@@ -182,7 +182,7 @@ __device__ __forceinline__ void det_table(const ConvParams& p, unsigned char* sm
     t.gx[r] = (float)gx;
     t.gy[r] = (float)gy;
   }
-  if (tid < 8) t.anc[tid] = p.anchor[tid];
+  if (ANC && tid < 8) t.anc[tid] = p.anchor[tid];
 }
 
 // Step 1 (registers): sigmoid of every logit, the Detect decode for the 4 box columns in the
@@ -267,7 +267,8 @@ __device__ __forceinline__ void det_epilogue(const ConvParams& p, unsigned char*
   det_table<BM, BN, NTH>(p, smem, m0, tid);
   __syncthreads();
   const bool std85 = p.no == 85 && p.na == 3;
-  if (std85) det_stage<BM, BN, TN, TM, 85, 3>(p, smem, acc, m0, wm, wn, g, li);
+  if (p.variant == 95) {}   // microbenchmark hook (with 94's empty K loop): no sigmoid / decode staging
+  else if (std85) det_stage<BM, BN, TN, TM, 85, 3>(p, smem, acc, m0, wm, wn, g, li);
   else det_stage<BM, BN, TN, TM, 0, 0>(p, smem, acc, m0, wm, wn, g, li);
   __syncthreads();
   if (p.variant == 93) {   // microbenchmark hook: no z / row-score stores
@@ -358,7 +359,10 @@ __device__ __forceinline__ void det_tail(const ConvParams& p, unsigned char* sme
       const long long z0 = t.zrow0[grp * 4];
       const f4 v = reinterpret_cast<const f4*>(zs + (a * BM + grp * 4) * NO)[c];
       if (z0 >= 0 && t.zrow0[grp * 4 + 3] == z0 + 3 && ((z0 + aoff) & 3) == 0) {
-        __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p.z + (size_t)(z0 + aoff) * NO) + c);
+        if (p.variant == 96)   // microbenchmark hook (with 94's empty K loop): temporal z stores
+          reinterpret_cast<f4*>(p.z + (size_t)(z0 + aoff) * NO)[c] = v;
+        else
+          __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p.z + (size_t)(z0 + aoff) * NO) + c);
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -369,6 +373,266 @@ __device__ __forceinline__ void det_tail(const ConvParams& p, unsigned char* sme
       }
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Persistent Detect head (round 3): the head conv + decode of one level (yolo.py:42-63) for the
+// standard head (na = 3, no = 85, 1x1, K = cin a multiple of 64, level size a multiple of 4, no raw
+// logits).  Measured on the tile kernel (scripts/detbench.hip hooks 90/93/94/95): at 80^2 its GEMM,
+// staging, row scores and z stores take 37 + 27 + 9 + 54 us and do not overlap — both blocks of a CU
+// run the same phase at the same time, so the z stores (209 MB at 80^2) drain while nothing else runs.
+// Here one block per CU walks 64-pixel tiles with the K-step ring running across tiles:
+//  * 8 waves (2 x 4), 64 pixels x 256 channels per tile, two 40 KiB ring stages + the z staging
+//    image (zs, the tile's z rows in z's layout) and the row table: 146 KiB of LDS;
+//  * the tile epilogue (sigmoid / decode into zs, row scores, z + row-record stores) runs after the
+//    K loop; its first barrier frees the ring, so the next tile's first TWO stages are issued before
+//    the epilogue and its K loop starts with both landed;
+//  * every wave issues the same stores in every tile (10 with row records: 2 record + 8 z stores per
+//    wave; rows past M, lanes without work and the other 3 lanes of a row's record go to an offset past
+//    the buffer range, where the store is dropped), so the epilogue's stores stay in flight behind
+//    counted vmcnt waits — they drain under the next tile's K loop and epilogue instead of stalling it.
+// Same arithmetic as det_stage / det_tail (bit-identical z and records).
+template <int BM, int NTH>
+__device__ __forceinline__ void det_tail_fixed(const ConvParams& p, unsigned char* smem, int tid,
+                                               __amdgpu_buffer_rsrc_t zr, __amdgpu_buffer_rsrc_t br, long long zb) {
+  constexpr int NO = 85, NA = 3, BN = 256;
+  const DetTab t = det_tab_ptrs<BM, BN>(smem);
+  const float* zs = reinterpret_cast<const float*>(smem);
+  const int hw = p.Ho * p.Wo;
+  float* zw = reinterpret_cast<float*>(smem);
+#pragma unroll
+  for (int t0 = 0; t0 < BM * NA * 4; t0 += NTH) {
+    // task (row r = anchor a x pixel pr, part): box column `part` of the row (the Detect decode in
+    // det_stage's op order, yolo.py:52-57) and a quarter of its row-score scan
+    const int tt = t0 + tid;
+    const int r = tt >> 2, part = tt & 3;
+    const int pr = r % BM, a = r / BM;
+    const bool inr = r < BM * NA;
+    const bool live = inr && t.zrow0[pr] >= 0;
+    if (inr) {
+      const float sgv = zs[r * NO + part];
+      const float t2 = sgv * 2.0f;
+      const float xy = (t2 - 0.5f + (part == 0 ? t.gx[pr] : t.gy[pr])) * p.stride;
+      const float wh = (t2 * t2) * t.anc[2 * a + (part == 3 ? 1 : 0)];
+      zw[r * NO + part] = part < 2 ? xy : wh;
+    }
+    if (p.best) {
+      const float* sg = zs + (live ? r : 0) * NO;
+      float best;
+      int bc;
+      det_best_lane<80>(sg, NO - 5, part, best, bc);
+#pragma unroll
+      for (int d = 1; d < 4; d <<= 1) {
+        const float ob = __shfl_xor(best, d, 64);
+        const int oc = __shfl_xor(bc, d, 64);
+        if (ob > best || (ob == best && oc < bc)) { best = ob; bc = oc; }
+      }
+      f4 rec;
+      rec[0] = sg[4];
+      rec[1] = best;
+      rec[2] = __builtin_bit_cast(float, bc);
+      rec[3] = 0.0f;
+      const uint32_t off = (live && part == 0) ? (uint32_t)((t.zrow0[pr] - zb + (long long)a * hw) * 16) : 0xffffffffu;
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, rec), br, off, 0, 2);   // nt
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // decoded box columns visible to the z stores
+  __builtin_amdgcn_s_barrier();
+  constexpr int G = BM / 4;            // 4-row groups per anchor
+  constexpr int GPP = NTH / NO;        // groups in flight per pass
+  constexpr int IT = (NA * G + GPP - 1) / GPP;
+  const int c = tid % NO, gg = tid / NO;
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int idx = gg + GPP * k;
+    const bool valid = gg < GPP && idx < NA * G;
+    const int ii = valid ? idx : 0;
+    const int a = ii / G, grp = ii - a * G;
+    const long long z0 = t.zrow0[grp * 4];
+    const f4 v = reinterpret_cast<const f4*>(zs + (a * BM + grp * 4) * NO)[c];
+    const uint32_t off = (valid && z0 >= 0) ? (uint32_t)((z0 - zb + (long long)a * hw) * NO * 4 + c * 16) : 0xffffffffu;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), zr, off, 0, 2);       // nt
+  }
+}
+
+template <int HOOK = 0>
+__global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams p) {
+  constexpr int BM = 64, BN = 256, WM = 2, WN = 4, NW = 8, NTH = 512;
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+  constexpr int RB = BN / 8 / NW;                  // 4 weight wave-instructions per stage (A: 1)
+  constexpr int PER = 1 + RB;
+  constexpr int STAGE = (BM + BN) * ROWB;          // 40 KiB
+  constexpr int RING = 2 * STAGE;
+  constexpr int LDS = RING + det_lds(BM, BN);
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
+  unsigned char* es = smem + RING;                 // zs + row table
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, li = lane & 15;
+  const int T = (p.M + BM - 1) / BM;
+  const int nk = p.kpad / BKE;
+  const TileWalk tw = xcd_tile_walk(T);
+  const int ntl = tw.count();
+  if (ntl == 0) return;
+
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto wr = make_rsrc(p.w, p.wbytes);
+  const int lr = lane >> 3;
+  const int c = (lane & 7) ^ lr;
+  uint32_t b_off[RB];
+#pragma unroll
+  for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)((((j * NW + wave) * 8 + lr) * p.kpad + c * 8) * 2);
+  const int hw = p.Ho * p.Wo;
+  auto a_off = [&](int it) -> uint32_t {
+    if (it >= ntl) return OOB;
+    const int m = tw.at(it) * BM + wave * 8 + lr;
+    if (m >= p.M) return OOB;
+    const int b = m / hw, cell = m - b * hw, ho = cell / p.Wo, wo = cell - ho * p.Wo;
+    return (uint32_t)((pix_index(b, ho, wo, p.H, p.W) * p.xc + p.xoff + c * 8) * 2);
+  };
+  // stage q = (tile it, K step k) into slot q & 1
+  int i_it = 0, i_k = 0, i_q = 0;
+  uint32_t i_aoff = a_off(0);
+  auto issue = [&]() __attribute__((always_inline)) {
+    unsigned char* As = smem + (i_q & 1) * STAGE;
+    unsigned char* Bs = As + BM * ROWB;
+    const bool live = i_it < ntl;
+    const uint32_t so = (uint32_t)i_k * BKE * 2;
+    dma16(xr, As + wave * 8 * ROWB, i_aoff, so);
+#pragma unroll
+    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * 8 * ROWB, live ? b_off[j] : OOB, so);
+    asm volatile("" ::: "memory");
+    ++i_q;
+    if (++i_k == nk) {
+      i_k = 0;
+      ++i_it;
+      i_aoff = a_off(i_it);
+    }
+  };
+
+  const f4 bias0 = {0.0f, 0.0f, 0.0f, 0.0f};
+  f4 bv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wn * WTN + j * 16 + g * 4;
+    bv[j] = bias0;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bv[j][e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
+  }
+  const int nst = p.best ? 10 : 8;   // epilogue stores per wave per tile (det_tail_fixed)
+
+  // z slot of each of this lane's 16 channels (j, e) in the tile's [na][BM][no] image (tile-invariant;
+  // the padding channel 255 -> a spare slot)
+  constexpr int NO = 85, NA = 3;
+  int zo[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ch = wn * WTN + j * 16 + g * 4 + e;
+      const int ca = ch / NO;
+      zo[j][e] = ca < NA ? ca * BM * NO + (ch - ca * NO) : NA * BM * NO;
+    }
+  // the level's anchors once (a per-lane kernel-argument load: its wait stays out of the tile loop)
+  if (tid < 8) det_tab_ptrs<BM, BN>(es).anc[tid] = p.anchor[tid];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  issue();
+  issue();
+  for (int it = 0; it < ntl; ++it) {
+    const int m0 = tw.at(it) * BM;
+    f4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = bv[j];
+    for (int k = 0; k < nk; ++k) {
+      // stage (it, k) landed: younger are stage (it, 1) and the previous epilogue's stores at k = 0,
+      // the previous epilogue's stores at k = 1 (both stages of a tile start are issued before them)
+      if (k == 0) {
+        if (it > 0 && nst == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 10) : "memory");
+        else if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 8) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+      } else if (k == 1 && it > 0) {
+        if (nst == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      if (k >= 1) issue();              // stage (it, k + 1) or the next tile's first stage
+      if (k == 0) det_table<BM, BN, NTH, false>(p, es, m0, tid);   // read after the K loop's last barrier
+      const unsigned char* As = smem + ((it * nk + k) & 1) * STAGE;
+      const unsigned char* Bs = As + BM * ROWB;
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const int ch = s * 4 + g;
+        u4 xa[TM], wb[TN];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = wm * WTM + i * 16 + li;
+          xa[i] = *reinterpret_cast<const u4*>(As + row * ROWB + swz(row, ch) * 16);
+        }
+#pragma unroll
+        for (int j = 0; j < TN; ++j) {
+          const int row = wn * WTN + j * 16 + li;
+          wb[j] = *reinterpret_cast<const u4*>(Bs + row * ROWB + swz(row, ch) * 16);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]),
+                                                               __builtin_bit_cast(h8, xa[i]), acc[j][i], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // epilogue: ring reads done -> the next tile's stage (it + 1, 1) into the free slot
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue();
+    if constexpr (HOOK != 1) {
+      // staging: the sigmoid of every logit into zs (z's layout); the 4 box columns of each row are
+      // decoded in det_tail_fixed (one (row, column) per thread there, beside the row scores)
+      float* zs = reinterpret_cast<float*>(es);
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int roff = (wm * WTM + i * 16 + li) * NO;
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) zs[zo[j][e] + (zo[j][e] < NA * BM * NO ? roff : 0)] = det_sig(acc[j][i][e]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // z / record rows of this tile relative to its first pixel's row (offsets stay 32-bit at any batch)
+    const int mb = m0 / hw;
+    const long long zb = (long long)mb * p.nrows + p.row_off + (m0 - mb * hw);
+    const auto zr = make_rsrc(p.z + (size_t)zb * 85, 0x7fffffffu);
+    const auto br = make_rsrc(p.best ? p.best + (size_t)zb * 4 : p.z, 0x7fffffffu);
+    det_tail_fixed<BM, NTH>(p, es, tid, zr, br, zb);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+bool det_pring_supported(const ConvParams& p) {
+  const int hw = p.Ho * p.Wo;
+  return p.k == 1 && p.s == 1 && p.na == 3 && p.no == 85 && p.cout == 255 && p.raw == nullptr &&
+         p.kpad == p.cin && p.cin % BKE == 0 && p.cin >= 2 * BKE && hw % 4 == 0 && p.row_off % 4 == 0 &&
+         p.nrows % 4 == 0 && p.xoff % 8 == 0 && p.xc % 8 == 0 && p.H == p.Ho && p.W == p.Wo;
+}
+
+hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
+  const long T = (p.M + 63) / 64;
+  const long per = (T + cus - 1) / cus;
+  const int grid = (int)((T + per - 1) / per);
+  if (p.variant == 98) YV7_LAUNCH(conv_det_pring_kernel<1>, dim3(grid), dim3(512), 0, st, p);
+  else YV7_LAUNCH(conv_det_pring_kernel<0>, dim3(grid), dim3(512), 0, st, p);
+  return hipGetLastError();
 }
 
 // 2x2 max of four 16-byte fp16 vectors (MP folded into a 1x1 conv's operand loads)
@@ -730,7 +994,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
     if (s0 < nk) issue(s0, s0);
 
   int slot = 0;
-  for (int kt = 0; kt < (DET && p.variant == 94 ? 0 : nk); ++kt) {
+  for (int kt = 0; kt < (DET && p.variant >= 94 && p.variant <= 96 ? 0 : nk); ++kt) {
     // stage kt must have landed; the (at most STAGES-2) stages issued after it may stay in flight
     const int ahead = nk - 1 - kt;
     if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
@@ -2291,7 +2555,11 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     }
   }
   if (det) {
-    // Detect head: BN = 256 covers the na*no = 255 channels of a pixel
+    // Detect head: the persistent head (conv_det_pring_kernel) where it applies; 98 = its
+    // microbenchmark hook (no staging), 99 = the 64 x 256 ring below (the round-2 default)
+    static const int det_pring = [] { const char* e = getenv("YV7_DET_PRING"); return e ? atoi(e) : 1; }();
+    if (((variant == 0 && det_pring) || variant == 98) && det_pring_supported(p)) return launch_det_pring(p, device_cus(), st);
+    // BN = 256 covers the na*no = 255 channels of a pixel
     // (scripts/detbench.hip, bs 32, row scores on: 64 x 256 ring, 2 blocks per CU so one block's
     // epilogue runs beside the other's main loop: 124 / 42 / 25 us at 80 / 40 / 20; 128 x 256 ring
     // 127 / 42 / 29; register-staged 64 x 256 tile 141 / 47 / 30)

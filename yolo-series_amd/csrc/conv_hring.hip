@@ -479,10 +479,14 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring2_kernel(const ConvParams
     const uint32_t off = (live && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
     __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
   };
-  static_assert(TN == 4 && TM == 4, "8 epilogue units over the next tile's first 6 phases");
-  // units of the previous tile carried by phase k = 0..5 of the next one: 0-1, 2-3, 4, 5, 6, 7
-  constexpr int UNIT0[6] = {0, 2, 4, 5, 6, 7};
-  constexpr int UNITN[6] = {2, 2, 1, 1, 1, 1};
+  static_assert(TN == 4 && TM == 4, "8 epilogue units per tile");
+  // a phase's epilogue share E = first unit * 4 + unit count (-1: none)
+  using E02 = std::integral_constant<int, 0 * 4 + 2>;
+  using E22 = std::integral_constant<int, 2 * 4 + 2>;
+  using E41 = std::integral_constant<int, 4 * 4 + 1>;
+  using E51 = std::integral_constant<int, 5 * 4 + 1>;
+  using E61 = std::integral_constant<int, 6 * 4 + 1>;
+  using E71 = std::integral_constant<int, 7 * 4 + 1>;
 
   uint32_t a_lane[3];
 #pragma unroll
@@ -530,10 +534,10 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring2_kernel(const ConvParams
     // the previous tile's epilogue units ride in the read segments (this group's reads are in flight,
     // the other group is in its MFMA segment): VALU beside the other wave's MFMAs, stores after this
     // phase's DMA issue
-    constexpr int NU = (EPI >= 0 && HOOK != 3) ? UNITN[EPI < 0 ? 0 : EPI] : 0;
+    constexpr int NU = (EPI >= 0 && HOOK != 3) ? (EPI & 3) : 0;
     if constexpr (NU > 0) {
 #pragma unroll
-      for (int u = 0; u < NU; ++u) epi_unit(prev, pt, UNIT0[EPI] + u, hp);
+      for (int u = 0; u < NU; ++u) epi_unit(prev, pt, (EPI >> 2) + u, hp);
     }
     // vmcnt: ops younger than the stages the next phase reads (issued last phase, see above) = last
     // phase's patch piece and epilogue stores, this phase's 3 weight pieces, patch piece and stores
@@ -575,12 +579,12 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring2_kernel(const ConvParams
     using I2 = std::integral_constant<int, 2>;
     using N = std::integral_constant<int, -1>;
     init_tile(acc, t);
-    phase(I0{}, std::integral_constant<int, 0>{}, acc, prev, pt, hp);
-    phase(I1{}, std::integral_constant<int, 1>{}, acc, prev, pt, hp);
-    phase(I2{}, std::integral_constant<int, 2>{}, acc, prev, pt, hp);
-    phase(I0{}, std::integral_constant<int, 3>{}, acc, prev, pt, hp);
-    phase(I1{}, std::integral_constant<int, 4>{}, acc, prev, pt, hp);
-    phase(I2{}, std::integral_constant<int, 5>{}, acc, prev, pt, hp);
+    phase(I0{}, E02{}, acc, prev, pt, hp);
+    phase(I1{}, E22{}, acc, prev, pt, hp);
+    phase(I2{}, E41{}, acc, prev, pt, hp);
+    phase(I0{}, E51{}, acc, prev, pt, hp);
+    phase(I1{}, E61{}, acc, prev, pt, hp);
+    phase(I2{}, E71{}, acc, prev, pt, hp);
     for (int c = 2; c < nch; ++c) {
       phase(I0{}, N{}, acc, prev, pt, hp);
       phase(I1{}, N{}, acc, prev, pt, hp);
