@@ -28,6 +28,8 @@
 // DMA, 14 no epilogue, 16 MFMA loop only.
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "yv7_kernels.h"
 
 namespace yv7 {
@@ -51,10 +53,12 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint3
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, vo, so, 0, 0);
 }
 
-// SCHED: 0 = the MFMA / ds_read / VALU issue pattern below (1 = no scheduling directives, 2 = MFMA /
-// ds_read interleave only, 3 = pattern + s_setprio around the MFMAs: round-2 experiments, all slower,
-// profiles/r2_ws64_sched_tune.txt; no longer launched)
-template <int ACT, int SCHED = 0>
+// HOOK: microbenchmark builds only (scripts/convbench.hip; the ABI never accepts them) — 12 no output
+// stores, 13 no patch DMA, 14 no epilogue, 16 MFMA loop only.  Compile-time, so that the production
+// form has no runtime test between the MFMAs and the previous tile's epilogue: a branch there puts the
+// epilogue in its own basic block, which the sched_group_barrier pattern cannot interleave with the
+// MFMAs (round 3: the epilogue then ran as a VALU block between super-steps, ~20 % of the kernel).
+template <int ACT, int HOOK = 0>
 __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
   unsigned char* wl = smem + 2 * PBUF;
@@ -108,7 +112,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
   auto issue_patch = [&](int t, int buf) {
     const uint32_t so = __builtin_amdgcn_readfirstlane(patch_origin(t));
     unsigned char* base = smem + buf * PBUF;
-    if (p.variant != 13 && p.variant != 16)
+    if constexpr (HOOK != 13 && HOOK != 16)
 #pragma unroll
       for (int k = 0; k < GPW; ++k) dma16(xr, base + dgrp[k] * 1024, dvo[k], so);
   };
@@ -136,27 +140,37 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
   // serves all three tap rows.  The next super-step's 18 fragments are read into the other register
   // set before this one's MFMAs, so LDS latency hides under 768 MFMA cycles; `side(ss)` runs after
   // super-step ss's MFMAs are issued (the previous tile's epilogue rides there).
-  auto load_ss = [&](const unsigned char* pb, int ss, u4 (&wf)[3][4], u4 (&xf)[6]) {
+  auto load_w = [&](int ss, u4 (&wf)[3][4]) __attribute__((always_inline)) {
     const int sc = ss >> 1, sub = ss & 1;
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
         wf[r][j] = *reinterpret_cast<const u4*>(wl + (r * 3 + sc) * WTAP + j * 16 * 128 + wbase[sub]);
+  };
+  auto load_x = [&](const unsigned char* pb, int ss, u4 (&xf)[6]) __attribute__((always_inline)) {
+    const int sc = ss >> 1, sub = ss & 1;
 #pragma unroll
     for (int q = 0; q < 6; ++q) xf[q] = *reinterpret_cast<const u4*>(pb + q * PS * 128 + pbase[sc][sub]);
   };
-  auto tile_mfma = [&](const unsigned char* pb, f4 (&acc)[4][4], auto&& side) {
-    u4 wA[3][4], xA[6], wB[3][4], xB[6];
-    load_ss(pb, 0, wA, xA);
-#pragma unroll
-    for (int ss = 0; ss < 6; ++ss) {
+  // Super-step ss computes from set (ss & 1); set 0's weights (tap column 0, K half 0) are the same
+  // for every tile, so the last super-step of a tile re-reads them for the next tile: at a tile's
+  // start only the 6 patch fragments wait on LDS behind the barrier.
+  u4 wA[3][4], xA[6], wB[3][4], xB[6];   // set 0's weights are first read after the first barrier
+  auto tile_mfma = [&](const unsigned char* pb, f4 (&acc)[4][4], auto&& side) __attribute__((always_inline)) {
+    load_x(pb, 0, xA);
+    auto step = [&](auto ssc) __attribute__((always_inline)) {
+      constexpr int ss = decltype(ssc)::value;
       auto& wc = (ss & 1) ? wB : wA;
       auto& xc = (ss & 1) ? xB : xA;
       auto& wn = (ss & 1) ? wA : wB;
       auto& xn = (ss & 1) ? xA : xB;
-      if (ss + 1 < 6) load_ss(pb, ss + 1, wn, xn);
-      if constexpr (SCHED == 3) __builtin_amdgcn_s_setprio(1);
+      if constexpr (ss + 1 < 6) {
+        load_w(ss + 1, wn);
+        load_x(pb, ss + 1, xn);
+      } else {
+        load_w(0, wn);
+      }
 #pragma unroll
       for (int r = 0; r < 3; ++r)
 #pragma unroll
@@ -165,20 +179,25 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
           for (int i = 0; i < 4; ++i)
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wc[r][j]),
                                                                __builtin_bit_cast(h8, xc[i + r]), acc[j][i], 0, 0, 0);
-      if constexpr (SCHED == 3) __builtin_amdgcn_s_setprio(0);
-      side(ss);
-      // issue pattern of the super-step: the next set's 18 fragment reads ride between the first 18
-      // MFMAs (their latency hides under the other 30), the side work's VALU ops two per MFMA
-      if constexpr (SCHED != 1) {
+      side(ssc);
+      // issue pattern of the super-step: the next set's fragment reads (18, or the 12 weight
+      // fragments of the next tile's first set) ride between the first MFMAs (their latency hides
+      // under the rest), the side work's VALU ops two per MFMA
+      constexpr int NR = ss + 1 < 6 ? 18 : 12;
 #pragma unroll
-        for (int k = 0; k < 48; ++k) {
-          __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
-          if (k < 18 && ss + 1 < 6) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
-          if constexpr (SCHED != 2) __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
-        }
-        __builtin_amdgcn_sched_barrier(0);
+      for (int k = 0; k < 48; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (k < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
       }
-    }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 5>{});
   };
   // epilogue piece q (0..7) of a finished tile: pixel row i = q / 2, channel pair (ja, jb) =
   // (2m, 2m+1), m = q % 2.  acc[j][i] holds channels j*16 + g*4 .. +3 of pixel (4*wave + i, li);
@@ -200,7 +219,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
     const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
     const u4 v = {s0[0], s1[0], s0[1], s1[1]};
-    if (p.variant != 12)
+    if constexpr (HOOK != 12)
       __builtin_amdgcn_raw_buffer_store_b128(v, yr, o0 + i * rowb + m * 64 + lane_ch, 0, 0);
   };
   auto init_acc = [&](f4 (&acc)[4][4]) {
@@ -230,7 +249,8 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
   __builtin_amdgcn_s_barrier();
   if (t + TS_ < TE) issue_patch(t + TS_, 1);
   init_acc(accA);
-  tile_mfma(smem, accA, [](int) {});
+  load_w(0, wA);   // (the weight image is complete: every wave's ds_writes precede the barrier)
+  tile_mfma(smem, accA, [](auto) {});
   oprev = out_origin(t);
   t += TS_;
   buf = 1;
@@ -240,10 +260,15 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     if (stores_out) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stores_out = true;
-    if (p.variant != 16) __builtin_amdgcn_s_barrier();
+    if constexpr (HOOK != 16) __builtin_amdgcn_s_barrier();
     if (t + TS_ < TE) issue_patch(t + TS_, buf ^ 1);
     init_acc(accB);
-    tile_mfma(smem + buf * PBUF, accB, [&](int ss) { if (p.variant != 14 && p.variant != 16) for (int q = (ss * 4) / 3; q < ((ss + 1) * 4) / 3; ++q) epi_piece(accA, oprev, q); });
+    tile_mfma(smem + buf * PBUF, accB, [&](auto ssc) __attribute__((always_inline)) {
+      constexpr int ss = decltype(ssc)::value;
+      if constexpr (HOOK != 14 && HOOK != 16)
+#pragma unroll
+        for (int q = (ss * 4) / 3; q < ((ss + 1) * 4) / 3; ++q) epi_piece(accA, oprev, q);
+    });
     oprev = out_origin(t);
     t += TS_;
     buf ^= 1;
@@ -254,16 +279,291 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
       return;
     }
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
-    if (p.variant != 16) __builtin_amdgcn_s_barrier();
+    if constexpr (HOOK != 16) __builtin_amdgcn_s_barrier();
     if (t + TS_ < TE) issue_patch(t + TS_, buf ^ 1);
     init_acc(accA);
-    tile_mfma(smem + buf * PBUF, accA, [&](int ss) { if (p.variant != 14 && p.variant != 16) for (int q = (ss * 4) / 3; q < ((ss + 1) * 4) / 3; ++q) epi_piece(accB, oprev, q); });
+    tile_mfma(smem + buf * PBUF, accA, [&](auto ssc) __attribute__((always_inline)) {
+      constexpr int ss = decltype(ssc)::value;
+      if constexpr (HOOK != 14 && HOOK != 16)
+#pragma unroll
+        for (int q = (ss * 4) / 3; q < ((ss + 1) * 4) / 3; ++q) epi_piece(accB, oprev, q);
+    });
     oprev = out_origin(t);
     t += TS_;
     buf ^= 1;
   }
 #pragma unroll
   for (int q = 0; q < 8; ++q) epi_piece(accA, oprev, q);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+
+// ---------------------------------------------------------------------------------------------
+// Half-patch ring form (variant 15; YV7_WS64R=1 makes it the dispatch's choice).  Measured on the
+// kernel above (scripts/convbench.hip, bs 32, round 3): at 320^2 the MFMA loop alone runs 177 us but
+// the whole kernel 330-340 — each CU keeps at most ONE 41 KiB patch in flight (the second LDS buffer
+// is the one being computed on), issued in a burst at the tile start and waited for at the next, so
+// the ~1.3 GB a layer moves runs at under 3 TB/s: latency-bound, not bandwidth-bound.  Here:
+//  * the patch is split by 32-channel K half into half-patches (324 pixels x 64 B, 21 DMA pieces of
+//    1 KiB) in a 4-slot LDS ring (84 KiB + the 72 KiB weight image): a tile's super-steps run K half 0
+//    (tap columns 0, 1, 2) then K half 1, so a half-patch is dead after its three super-steps;
+//  * one ring step per half: before the half's LAST super-step (its fragments are already in
+//    registers) wait for the next half-patch, barrier, and refill the slot just finished with the
+//    half-patch four ahead — three half-patches (62 KiB) stay in flight continuously and each lands
+//    ~3 halves (~430 MFMA cycles x 3) after it was issued;
+//  * the last super-step of a half prefetches the next half's first fragments (after the barrier),
+//    so a tile start no longer waits on LDS; set 0's weights are re-read for the next tile there too;
+//  * every wave issues 6 DMA pieces per half (waves 1-3 duplicate wave 0's piece 20: identical bytes,
+//    distinct per-wave issue) and 4 epilogue stores per half (1, 2, 1 over its super-steps), so every
+//    counted vmcnt is a compile-time constant once the ring is full (24); the block's first tile
+//    stores into the void (offsets past the buffer range) to keep the count.
+// LDS: 4 x 21 KiB + 72 KiB = 156 KiB.  Slots are compile-time: one loop trip = 2 tiles = 4 halves.
+// Measured (round 3, profiles/r3p/): convbench (random operands, input not cache-resident)
+// @320 330 us vs 296 for the column-pair form with its epilogue interleaved, @160 74 vs 82; in-network
+// (tune_ops, one layer forced) equal within 1-2 us on every layer — the deeper ring does not buy
+// bandwidth at 320^2 (64-B half-lines per pixel: twice the L2 requests per byte of the 128-B lines
+// the column-pair form fetches), so it is kept as an alternative, not the default.
+template <int ACT>
+__global__ __launch_bounds__(NT, 1) void conv3x3_ws64r_kernel(const ConvParams p) {
+  constexpr int HP = 21 * 1024;              // one half-patch slot (336 rows of 64 B)
+  constexpr int WOFF = 4 * HP;
+  constexpr int NP = 6;                      // DMA pieces per wave per half
+  constexpr int ROW = 64;                    // bytes per patch pixel row in a slot (32 channels)
+  constexpr uint32_t DUMMY_SO = 0x40000000u; // scalar offset of a half-patch past the walk: reads zeros
+  constexpr int BOFF = WOFF + 9 * WTAP;     // 64 fp32 biases
+  static_assert(BOFF + CO * 4 <= 160 * 1024, "LDS budget");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[BOFF + CO * 4];
+  unsigned char* wl = smem + WOFF;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int tx_n = p.W / TS, tpi = tx_n * (p.H / TS), T = p.B * tpi;
+  const TileWalk tw = xcd_tile_walk(T);
+  const int ntl = tw.count();
+  if (ntl == 0) return;
+
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto yr = make_rsrc(p.y, 0x7fffffffu);
+
+  // bias in LDS (registers are the scarce resource here: two accumulator and fragment sets)
+  float* bias_l = reinterpret_cast<float*>(smem + BOFF);
+  if (tid < CO) bias_l[tid] = p.bias[tid];
+
+  // weights -> LDS once (the layout of the kernel above)
+  {
+    const unsigned char* w = reinterpret_cast<const unsigned char*>(p.w);
+    for (int q = tid; q < 9 * CO * 8; q += NT) {
+      const int t = q / (CO * 8), rem = q - t * CO * 8, n = rem >> 3, slot = rem & 7;
+      const int chunk = slot ^ (n & 7);
+      const u4 v = *reinterpret_cast<const u4*>(w + ((size_t)n * p.kpad + t * CI + chunk * 8) * 2);
+      *reinterpret_cast<u4*>(wl + t * WTAP + n * 128 + slot * 16) = v;
+    }
+  }
+
+  // half-patch DMA: piece G = wave + 4k (k < 5), the sixth is piece 20 for every wave.  Lane l of piece
+  // G: patch pixel pp = 16 G + (l >> 2), LDS slot l & 3 of its 64-B row holds source chunk
+  // (l & 3) ^ ((px >> 1) & 3) (the reader's swizzle); offsets relative to the half's origin.
+  uint32_t dvo[NP], dlds[NP];
+#pragma unroll
+  for (int k = 0; k < NP; ++k) {
+    const int G = k < 5 ? wave + 4 * k : 20;
+    dlds[k] = (uint32_t)(G * 1024);
+    const int pp = 16 * G + (lane >> 2);
+    const int py = pp / PS, px = pp - py * PS;
+    const int c = (lane & 3) ^ ((px >> 1) & 3);
+    dvo[k] = pp < PPIX ? (uint32_t)(((py * (p.W + 2 * BORDER) + px) * p.xc + c * 8) * 2) : 0x80000000u;
+  }
+  auto origin = [&](int it) -> uint32_t {   // scalar byte offset of tile it's patch origin, channel 0
+    if (it >= ntl) return DUMMY_SO;
+    const int t = tw.at(it);
+    const int b = t / tpi, r = t - b * tpi, ty = r / tx_n, tx = r - ty * tx_n;
+    return __builtin_amdgcn_readfirstlane(
+        (uint32_t)((pix_index(b, ty * TS - 1, tx * TS - 1, p.H, p.W) * p.xc + p.xoff) * 2));
+  };
+  auto issue_half = [&](int slot, uint32_t so) __attribute__((always_inline)) {
+#pragma unroll
+    for (int k = 0; k < NP; ++k) dma16(xr, smem + slot * HP + dlds[k], dvo[k], so);
+    asm volatile("" ::: "memory");   // pin the DMA before this super-step's stores (the counted waits)
+  };
+
+  // fragment read bases: weights as the kernel above; patch pixel (4 wave + q, li + s) of a slot
+  // (ds_read offsets are 16-bit immediates: the weight image is addressed from two bases — taps 0-5
+  // and 6-8 — and slot 3 from its own, each laundered through an empty asm so the compiler cannot fold
+  // them back into one base plus offsets too large for the immediate, which it would then materialize
+  // as one VGPR per read and spill)
+  uint32_t wlo[2], whi[2], xl[3], xl3[3];
+#pragma unroll
+  for (int sub = 0; sub < 2; ++sub) {
+    const uint32_t wb = (uint32_t)(WOFF + li * 128 + (((sub * 4 + g) ^ (li & 7)) * 16));
+    wlo[sub] = wb;
+    whi[sub] = wb + 6 * WTAP;
+    asm volatile("" : "+v"(wlo[sub]));
+    asm volatile("" : "+v"(whi[sub]));
+  }
+#pragma unroll
+  for (int s = 0; s < 3; ++s) {
+    xl[s] = (uint32_t)((4 * wave * PS + li + s) * ROW + ((g ^ (((li + s) >> 1) & 3)) * 16));
+    xl3[s] = xl[s] + 3 * HP;
+    asm volatile("" : "+v"(xl[s]));
+    asm volatile("" : "+v"(xl3[s]));
+  }
+
+  const uint32_t rowb = (uint32_t)((p.Wo + 2 * BORDER) * p.yc * 2);
+  auto out_origin = [&](int it) -> uint32_t {
+    const int t = tw.at(it);
+    const int b = t / tpi, rr = t - b * tpi, ty = rr / tx_n, tx = rr - ty * tx_n;
+    return (uint32_t)((pix_index(b, ty * TS + 4 * wave, tx * TS + li, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
+  };
+  const uint32_t lane_ch = (uint32_t)((16 * (g & 1) + 8 * (g >> 1)) * 2);
+  auto epi_piece = [&](const f4 (&acc)[4][4], uint32_t o0, int q) __attribute__((always_inline)) {
+    const int i = q >> 1, m = q & 1;
+    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+    h4 va, vb;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      va[e] = (_Float16)act_t<ACT>(acc[2 * m][i][e]);
+      vb[e] = (_Float16)act_t<ACT>(acc[2 * m + 1][i][e]);
+    }
+    const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
+    const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
+    const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
+    const u4 v = {s0[0], s1[0], s0[1], s1[1]};
+    __builtin_amdgcn_raw_buffer_store_b128(v, yr, o0 + i * rowb + m * 64 + lane_ch, 0, 0);
+  };
+
+  u4 wA[3][4], xA[6], wB[3][4], xB[6];
+  auto load_w = [&](int s, int sub, u4 (&wf)[3][4]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        wf[r][j] = *reinterpret_cast<const u4*>(
+            smem + (r < 2 ? wlo[sub] + (r * 3 + s) * WTAP : whi[sub] + s * WTAP) + j * 16 * 128);
+  };
+  auto load_x = [&](int slot, int s, u4 (&xf)[6]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 6; ++q)
+      xf[q] = *reinterpret_cast<const u4*>(smem + (slot == 3 ? xl3[s] : xl[s] + slot * HP) + q * PS * ROW);
+  };
+
+  // vmcnt of ring step `pos` (0..3 within a loop trip): the ops younger than the half-patch the next
+  // half reads — two halves of DMA (12) and the stores since it was issued (12 once the ring is full;
+  // the first trip's first three steps follow the prologue: 3, 7, 11)
+  auto ring_wait = [&](auto posc, bool first) __attribute__((always_inline)) {
+    constexpr int pos = decltype(posc)::value;
+    if (pos < 3 && first) {
+      if constexpr (pos == 0) asm volatile("s_waitcnt vmcnt(15) lgkmcnt(0)" ::: "memory");
+      if constexpr (pos == 1) asm volatile("s_waitcnt vmcnt(19) lgkmcnt(0)" ::: "memory");
+      if constexpr (pos == 2) asm volatile("s_waitcnt vmcnt(23) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(24) lgkmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+  };
+
+  // one tile (slots S0 = K half 0, S0 + 1 = K half 1) into acc; prev / oprev: the previous tile's
+  // epilogue, 8 pieces over the six super-steps; so2: the origin of the tile two ahead (its halves
+  // refill this tile's slots)
+  auto run_tile = [&](auto s0c, f4 (&acc)[4][4], const f4 (&prev)[4][4], uint32_t oprev, uint32_t so2, bool first)
+      __attribute__((always_inline)) {
+    constexpr int S0 = decltype(s0c)::value;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const f4 bv = *reinterpret_cast<const f4*>(bias_l + j * 16 + g * 4);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) acc[j][i] = bv;
+    }
+    auto step = [&](auto ssc) __attribute__((always_inline)) {
+      constexpr int ss = decltype(ssc)::value;   // 0..5: K half ss / 3, tap column ss % 3
+      constexpr int sub = ss / 3, s = ss % 3;
+      auto& wc = (ss & 1) ? wB : wA;
+      auto& xc = (ss & 1) ? xB : xA;
+      auto& wn = (ss & 1) ? wA : wB;
+      auto& xn = (ss & 1) ? xA : xB;
+      if constexpr (s == 2) {
+        // ring step: the next half-patch landed everywhere; refill this half's slot
+        ring_wait(std::integral_constant<int, (S0 / 2) * 2 + sub>{}, first);
+        issue_half(S0 + sub, so2 + (uint32_t)(sub * 64));
+        __builtin_amdgcn_sched_barrier(0);
+        // next fragments: K half 1 column 0 of this tile, or the next tile's K half 0 column 0
+        load_w(0, 1 - sub, wn);
+        load_x(sub == 0 ? S0 + 1 : (S0 + 2) % 4, 0, xn);
+      } else {
+        load_w(s + 1, sub, wn);
+        load_x(S0 + sub, s + 1, xn);
+      }
+#pragma unroll
+      for (int r = 0; r < 3; ++r)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wc[r][j]),
+                                                               __builtin_bit_cast(h8, xc[i + r]), acc[j][i], 0, 0, 0);
+      // previous tile's epilogue: pieces (1, 2, 1) per K half
+      {
+        constexpr int q0 = sub * 4 + (s == 0 ? 0 : s == 1 ? 1 : 3);
+        constexpr int nq = s == 1 ? 2 : 1;
+#pragma unroll
+        for (int q = q0; q < q0 + nq; ++q) epi_piece(prev, oprev, q);
+      }
+      // issue pattern: the 18 next-fragment reads between the first MFMAs, epilogue VALU two per MFMA
+#pragma unroll
+      for (int k = 0; k < 48; ++k) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
+        if (k < 18) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
+        __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    };
+    step(std::integral_constant<int, 0>{});
+    step(std::integral_constant<int, 1>{});
+    step(std::integral_constant<int, 2>{});
+    step(std::integral_constant<int, 3>{});
+    step(std::integral_constant<int, 4>{});
+    step(std::integral_constant<int, 5>{});
+  };
+  auto last_epilogue = [&](const f4 (&acc)[4][4], uint32_t o) __attribute__((always_inline)) {
+#pragma unroll
+    for (int q = 0; q < 8; ++q) epi_piece(acc, o, q);
+  };
+
+  // prologue: halves 0..3 (tiles 0 and 1) into slots 0..3, then half 0 landed and the weight image
+  // complete everywhere; tile 0's first fragments
+  {
+    const uint32_t o0 = origin(0), o1 = origin(1);
+    issue_half(0, o0);
+    issue_half(1, o0 + 64);
+    issue_half(2, o1);
+    issue_half(3, o1 + 64);
+  }
+  asm volatile("s_waitcnt vmcnt(18) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  load_w(0, 0, wA);
+  load_x(0, 0, xA);
+
+  f4 accA[4][4], accB[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) accB[j][i] = f4{0.0f, 0.0f, 0.0f, 0.0f};
+  uint32_t oprev = 0x80000000u;   // the first tile's "previous tile" stores land past the buffer range
+  for (int it = 0;; it += 2) {
+    const bool first = it == 0;
+    run_tile(std::integral_constant<int, 0>{}, accA, accB, oprev, origin(it + 2), first);
+    oprev = out_origin(it);
+    if (it + 1 == ntl) {
+      last_epilogue(accA, oprev);
+      break;
+    }
+    run_tile(std::integral_constant<int, 2>{}, accB, accA, oprev, origin(it + 3), first);
+    oprev = out_origin(it + 1);
+    if (it + 2 == ntl) {
+      last_epilogue(accB, oprev);
+      break;
+    }
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -290,9 +590,28 @@ hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st) {
   if (!ws64_supported(p)) return hipErrorInvalidValue;
   const int T = p.B * (p.H / TS) * (p.W / TS);
   const int grid = T < num_cus() ? T : num_cus();
-  if (p.act == 1) YV7_LAUNCH((conv3x3_ws64_kernel<1>), dim3(grid), dim3(NT), 0, st, p);
-  else if (p.act == 2) YV7_LAUNCH((conv3x3_ws64_kernel<2>), dim3(grid), dim3(NT), 0, st, p);
-  else YV7_LAUNCH((conv3x3_ws64_kernel<0>), dim3(grid), dim3(NT), 0, st, p);
+  // microbenchmark hooks (scripts/convbench.hip only; the ABI never accepts them) on the column-pair form
+  if (p.act == 1 && p.variant >= 12 && p.variant <= 16 && p.variant != 15) {
+    if (p.variant == 12) YV7_LAUNCH((conv3x3_ws64_kernel<1, 12>), dim3(grid), dim3(NT), 0, st, p);
+    else if (p.variant == 13) YV7_LAUNCH((conv3x3_ws64_kernel<1, 13>), dim3(grid), dim3(NT), 0, st, p);
+    else if (p.variant == 14) YV7_LAUNCH((conv3x3_ws64_kernel<1, 14>), dim3(grid), dim3(NT), 0, st, p);
+    else YV7_LAUNCH((conv3x3_ws64_kernel<1, 16>), dim3(grid), dim3(NT), 0, st, p);
+    return hipGetLastError();
+  }
+  // the two forms measured equal in-network (scripts/tune_ops.py, one layer forced at a time, same box,
+  // us, 11 / 15: @320 228.2 / 228.4, @160 73.7 / 71.6, 71.4 / 69.8, 71.4 / 70.8, 72.3 / 71.1 — and the
+  // halo kernel keeps the @80 layers: 30.1 vs 32.2 / 34.1); the column-pair form stays the default.
+  // YV7_WS64R=1: the ring form.
+  static const int ring = [] { const char* e = getenv("YV7_WS64R"); return e ? atoi(e) : 0; }();
+  if (p.variant == 11 || (p.variant != 15 && !ring)) {
+    if (p.act == 1) YV7_LAUNCH((conv3x3_ws64_kernel<1>), dim3(grid), dim3(NT), 0, st, p);
+    else if (p.act == 2) YV7_LAUNCH((conv3x3_ws64_kernel<2>), dim3(grid), dim3(NT), 0, st, p);
+    else YV7_LAUNCH((conv3x3_ws64_kernel<0>), dim3(grid), dim3(NT), 0, st, p);
+    return hipGetLastError();
+  }
+  if (p.act == 1) YV7_LAUNCH((conv3x3_ws64r_kernel<1>), dim3(grid), dim3(NT), 0, st, p);
+  else if (p.act == 2) YV7_LAUNCH((conv3x3_ws64r_kernel<2>), dim3(grid), dim3(NT), 0, st, p);
+  else YV7_LAUNCH((conv3x3_ws64r_kernel<0>), dim3(grid), dim3(NT), 0, st, p);
   return hipGetLastError();
 }
 
