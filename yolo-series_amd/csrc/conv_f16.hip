@@ -2422,6 +2422,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (pcfg == 1) return launch_t<128, 128, 2, false, false, 1, true>(p, st);
     return launch_t<64, 128, 1, false, false, 1, true>(p, st);
   }
+  // the register-streamed 1x1 (conv_rs.hip; 240 forces it where it applies)
+  if (!det && variant == 240 && conv1x1_rs_supported(p, nullptr)) return launch_conv1x1_rs(p, nullptr, st);
   // the 3x3 halo ring (conv_hring.hip): 260 = 128-channel tiles, 261 = 256-channel tiles
   if (!det && (variant == 260 || variant == 261 || variant == 262 || (variant >= 911 && variant <= 914)) &&
       hring_supported(p))
@@ -2463,8 +2465,12 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
       return launch_pring_ws<128, 256, 2, 4, 4>(p, st);
     if (p8_default(p)) return launch_p8(p, one, st);
     if (one) {
-      if (p.K >= 256 && p.cout >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
-      if (wide && p.cout >= 256 && t256 >= 200) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
+      // (a cout that is not a multiple of 256 — the tensor-fused pair 512->256+128 @80 — would leave
+      // half of every last 256-wide N tile idle: the 128 x 128 ring below, 148.8 -> 124.2 us in-network,
+      // profiles/r3r/tune.txt)
+      const bool n256 = p.cout % 256 == 0 || p.K > 512;
+      if (n256 && p.K >= 256 && p.cout >= 256 && t256 >= 1600) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
+      if (n256 && wide && p.cout >= 256 && t256 >= 200) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
       if (p.K <= 512 && p.M >= 51200)
         return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     } else if (wide && p.k == 3 && p.cin >= 256 && p.cout >= 256 && t256 >= 200) {

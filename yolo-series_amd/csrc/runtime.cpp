@@ -362,7 +362,8 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (kind == YV7_OP_DETECT) return v == 92 || v == 97 || v == 99;
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
-  return (v >= 201 && v <= 206) || (v >= 211 && v <= 218) || (v >= 221 && v <= 223) || (v >= 231 && v <= 238) || (v >= 260 && v <= 262);
+  return (v >= 201 && v <= 206) || (v >= 211 && v <= 218) || (v >= 221 && v <= 223) || (v >= 231 && v <= 238) || v == 240 ||
+         (v >= 260 && v <= 262);
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {
@@ -494,6 +495,7 @@ static int forward_impl(yv7_plan* p, const void* x, int x_dtype, int B, int H, i
       }
       case YV7_OP_CONV:
       case YV7_OP_DETECT: {
+        if (fused_until > i) break;   // the second op of a dual 1x1 launch (below)
         yv7::ConvParams c = conv_params(p, i, B, H, W);
         c.x = wsb + off[o.src];
         c.w = wb + o.w_off;
@@ -551,6 +553,47 @@ static int forward_impl(yv7_plan* p, const void* x, int x_dtype, int B, int H, i
             f.act = o.act;
             e = yv7::launch_conv_f8(f, st);
             break;
+          }
+          // The MP block's two readers of one tensor (cfg/deploy/yolov7.yaml: `MP -> 1x1` and `1x1`,
+          // adjacent ops here: the pooled one is the fp16 plan's pool = 2 op) as ONE register-streamed
+          // launch that reads the tensor once (conv_rs.hip); the second op records no time of its own.
+          // Both ops on the default dispatch only; YV7_DUAL=0: off.
+          static const int dual = [] { const char* ev = getenv("YV7_DUAL"); return ev ? atoi(ev) : 1; }();
+          if (dual && p->dtype == YV7_DT_F16 && i + 1 < p->ops.size() && p->op_variant[i] == 0 &&
+              p->op_variant[i + 1] == 0) {
+            const auto& o1 = p->ops[i + 1];
+            const bool pair = o1.kind == YV7_OP_CONV && !is_f8(o1) && o1.src == o.src && o1.src_coff == o.src_coff &&
+                              o1.cin == o.cin && o1.k == 1 && o.k == 1 && ((o.pool == 2) != (o1.pool == 2)) &&
+                              o1.w_off != o.w_off;
+            if (pair) {
+              const size_t fi = o.pool == 2 ? i + 1 : i, pi = o.pool == 2 ? i : i + 1;
+              const auto& of = p->ops[fi];
+              const auto& op_ = p->ops[pi];
+              yv7::ConvParams cf = conv_params(p, fi, B, H, W);
+              cf.x = c.x;
+              cf.w = wb + of.w_off;
+              cf.bias = reinterpret_cast<const float*>(wb + of.b_off);
+              cf.zero = p->zero;
+              const auto& tf = p->tensors[of.dst];
+              const auto& tp = p->tensors[op_.dst];
+              cf.y = wsb + off[of.dst];
+              cf.yc = tf.channels;
+              cf.yoff = of.dst_coff;
+              yv7::Conv1x1Pooled q;
+              q.w = wb + op_.w_off;
+              q.bias = reinterpret_cast<const float*>(wb + op_.b_off);
+              q.y = wsb + off[op_.dst];
+              q.yc = tp.channels;
+              q.yoff = op_.dst_coff;
+              q.cout = op_.cout;
+              q.act = op_.act;
+              if (cf.Ho == (H >> tf.shift) && cf.Wo == (W >> tf.shift) && tp.shift == tf.shift + 1 &&
+                  yv7::conv1x1_rs_supported(cf, &q)) {
+                e = yv7::launch_conv1x1_rs(cf, &q, st);
+                fused_until = i + 2;
+                break;
+              }
+            }
           }
           e = yv7::launch_conv(p->dtype, c, false, st);
         } else {

@@ -138,6 +138,17 @@ struct ConvParams {
   int pool;           // 2: 1x1 conv over the 2x2 / stride-2 max of the input (MP folded in; k = 1, s = 2)
 };
 
+// The max-pooled second consumer of a register-streamed 1x1 conv's input (conv_rs.hip): the MP block's
+// `MP -> 1x1` branch (pool = 2 op) launched together with the plain 1x1 reading the same tensor.
+struct Conv1x1Pooled {
+  const void* w;        // packed weights [cout_pad32][kpad] (kpad == the full conv's)
+  const float* bias;
+  void* y;              // bordered NHWC output tensor at half resolution
+  int yc, yoff, cout, act;
+};
+bool conv1x1_rs_supported(const ConvParams& p, const Conv1x1Pooled* q);
+hipError_t launch_conv1x1_rs(const ConvParams& p, const Conv1x1Pooled* q, hipStream_t st);
+
 // Split-K scratch the fp16 dispatch needs for one conv (0 when it does not split).
 size_t conv_splitk_part_bytes(const ConvParams& p);
 int conv_splitk_tiles(const ConvParams& p);

@@ -380,6 +380,8 @@ def compile_model(model, dtype: int, fp8=None) -> Graph:
     folded = _fold_pools(g) if dtype == L.DT_F16 and os.environ.get('YV7_NO_POOLFOLD') != '1' else []
     if os.environ.get('YV7_NO_MERGE') != '1':
         _merge_siblings(g)
+        if os.environ.get('YV7_NO_TMERGE') != '1':
+            _merge_sibling_tensors(g, loc)
     fp8 = fp8 or {}
     for idx, o in enumerate(g.ops):
         if '_w' in o:
@@ -423,6 +425,94 @@ def _fold_pools(g: Graph):
         folded.append(mp.get('layer'))
         del g.ops[i]
     return folded
+
+
+def _overlaps(t, lo, n, t2, lo2, n2):
+    return t == t2 and lo < lo2 + n2 and lo2 < lo + n
+
+
+def _merge_sibling_tensors(g: Graph, loc: dict):
+    """Sibling CONVs that read the same input slice with the same geometry but write into DIFFERENT
+    tensors: when one writes the last channels of its tensor and the other the first channels of its
+    own, the two tensors become one ([first | second], every reference remapped) and the convs one GEMM
+    with N = cout_a + cout_b, as in _merge_siblings.  yolov7 (cfg/deploy/yolov7.yaml): layers 27 + 66
+    (the P3 output into the next MP block's 1x1 and into the head's P3 route `[24, 1, Conv, [128, 1,
+    1]]`), 40 + 54 (the same at P4) and SPPCSPC 51's cv1 + cv2 (models/common.py:271-280) — pairs of
+    launches that each re-read a 52-210 MB input at bs 32.  Only the layout changes (the
+    merged tensor's channel pitch); every layer's output keeps its values and its (tensor, offset) in
+    layer_tensor."""
+    key = ('src', 'src_coff', 'cin', 'k', 's', 'pad', 'act', 'pool')
+    i = 0
+    while i < len(g.ops):
+        a = g.ops[i]
+        if a['kind'] != L.OP_CONV or '_w' not in a:
+            i += 1
+            continue
+        merged = False
+        for j in range(i + 1, len(g.ops)):
+            b = g.ops[j]
+            wb = _writes(b)
+            if (b['kind'] == L.OP_CONV and '_w' in b and all(a.get(k) == b.get(k) for k in key) and
+                    b['dst'] != a['dst'] and g.tensors[a['dst']][1] == g.tensors[b['dst']][1]):
+                ca, cb = g.tensors[a['dst']][0], g.tensors[b['dst']][0]
+                if a['dst_coff'] + a['cout'] == ca and b['dst_coff'] == 0:
+                    first, second = a, b          # [a's tensor | b's tensor]
+                elif b['dst_coff'] + b['cout'] == cb and a['dst_coff'] == 0:
+                    first, second = b, a          # [b's tensor | a's tensor]
+                else:
+                    first = None
+                if first is not None:
+                    # b moves up to a's position: nothing in between may write b's input or read / write
+                    # b's output slice
+                    ok = True
+                    for o in g.ops[i + 1:j]:
+                        wo = _writes(o)
+                        if wo and (_overlaps(*wo, b['src'], b['src_coff'], b['cin']) or
+                                   _overlaps(*wo, b['dst'], b['dst_coff'], b['cout'])):
+                            ok = False
+                        if o.get('src', -1) >= 0 and _overlaps(o['src'], o.get('src_coff', 0),
+                                                               max(o.get('cin', 0), o.get('cout', 0)),
+                                                               b['dst'], b['dst_coff'], b['cout']):
+                            ok = False
+                    if ok:
+                        _fuse_tensors(g, loc, first['dst'], second['dst'])
+                        m = dict(a)
+                        m['dst'] = first['dst']
+                        m['dst_coff'] = first['dst_coff']
+                        m['cout'] = a['cout'] + b['cout']
+                        m['_w'] = torch.cat([first['_w'], second['_w']], 0)
+                        m['_b'] = torch.cat([first['_b'], second['_b']], 0)
+                        m['merged'] = (first['cout'], second['cout'])
+                        m['layers'] = first['layers'] + second['layers']
+                        g.ops[i] = m
+                        del g.ops[j]
+                        merged = True
+                        break
+            if wb and _overlaps(*wb, a['src'], a['src_coff'], a['cin']):
+                break  # a's input is overwritten from here on
+        if not merged:
+            i += 1
+
+
+def _fuse_tensors(g: Graph, loc: dict, t1: int, t2: int):
+    """Tensor t2 becomes channels [C1, C1 + C2) of tensor t1; t2's id is removed (higher ids shift down)
+    in every op and in the layer -> (tensor, offset) map."""
+    c1 = g.tensors[t1][0]
+    g.tensors[t1][0] = c1 + g.tensors[t2][0]
+
+    def remap(t, off):
+        if t == t2:
+            t, off = t1, off + c1
+        return (t - 1 if t > t2 else t), off
+
+    for o in g.ops:
+        if o.get('src', -1) >= 0:
+            o['src'], o['src_coff'] = remap(o['src'], o.get('src_coff', 0))
+        if o.get('dst', -1) >= 0:
+            o['dst'], o['dst_coff'] = remap(o['dst'], o.get('dst_coff', 0))
+    for k, (t, off) in list(loc.items()):
+        loc[k] = remap(t, off)
+    del g.tensors[t2]
 
 
 def _writes(o):
