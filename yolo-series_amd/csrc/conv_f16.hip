@@ -1101,7 +1101,10 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
 // WS > 0: weight-stationary 1x1 form — the layer's whole weight matrix (cout <= BN, K <= WS steps)
 // is DMA'd into LDS once per block and every tile's K steps read it from there, so only the
 // activation tile streams (a third of the DMA issue of the 256 x 256 ring); bias in registers.
-template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int ACT, int BK, int WS = 0>
+// HOOK (scripts/convbench.hip only, 256 x 256 form; the ABI never accepts them): 296 activation without
+// stores, 297 neither, 298 no operand DMA.  Compile-time: a runtime test in the K loop splits the DMA
+// issue into a block of its own on every K step of the production kernel.
+template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, int ACT, int BK, int WS = 0, int HOOK = 0>
 __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 1024 && WM * WN == 4) ? 3 : (STAGES * (BM + BN) * BK * 2 <= 76 * 1024) ? 2 : 1) void conv_f16_pring_kernel(
     const ConvParams p) {
   constexpr int NW = WM * WN, NTH = 64 * NW;
@@ -1184,7 +1187,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
     const int slot = ig % STAGES;
     unsigned char* As = smem + slot * STAGE;
     unsigned char* Bs = As + BM * RB_;
-    if (p.variant != 298) {   // 298: microbenchmark hook, no operand traffic (times the rest)
+    if constexpr (HOOK != 298) {   // 298: microbenchmark hook, no operand traffic (times the rest)
       aw.step(p, ikt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * RPI * RB_, vo, so); });
       if constexpr (WS == 0) {
 #pragma unroll
@@ -1221,14 +1224,14 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii) asm volatile("" : "+v"(acc[j][ii]));
-    if (p.variant == 296 || p.variant == 297) {   // microbenchmark hooks: 296 activation, no stores; 297 neither
+    if constexpr (HOOK == 296 || HOOK == 297) {   // microbenchmark hooks: 296 activation, no stores; 297 neither
       float sink = 0.0f;
 #pragma unroll
       for (int ii = 0; ii < TM; ++ii)
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) sink += p.variant == 297 ? acc[j][ii][e] : act_t<ACT>(acc[j][ii][e]);
+          for (int e = 0; e < 4; ++e) sink += HOOK == 297 ? acc[j][ii][e] : act_t<ACT>(acc[j][ii][e]);
       if (sink == 12345.0f) __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, sink), yr, 0, 0, 0);
       return;
     }
@@ -2178,6 +2181,15 @@ int device_cus() {
   return n;
 }
 
+template <int HOOK>
+hipError_t launch_pring_hook(const ConvParams& p, bool one, hipStream_t st) {
+  const long T = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
+  const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
+  if (one) YV7_LAUNCH((conv_f16_pring_kernel<256, 256, 2, 4, 2, true, 1, 64, 0, HOOK>), dim3(grid), dim3(512), 0, st, p);
+  else YV7_LAUNCH((conv_f16_pring_kernel<256, 256, 2, 4, 2, false, 1, 64, 0, HOOK>), dim3(grid), dim3(512), 0, st, p);
+  return hipGetLastError();
+}
+
 // the 8-phase persistent ring: uniform K steps only (1x1, or cin % 64 == 0)
 int env_variant() {
   static const int v = [] { const char* e = getenv("YV7_CONV_F16"); return e ? atoi(e) : 0; }();
@@ -2488,7 +2500,10 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   if (ch.cfg >= 0) return launch_choice(p, ch, one, st);
   if (!det && p.cout > 32) {
     // persistent ring configurations (microbenchmarks: 201..206)
-    if (variant == 201 || (variant >= 296 && variant <= 298)) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
+    if (variant == 201) return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
+    if (variant == 296) return launch_pring_hook<296>(p, one, st);
+    if (variant == 297) return launch_pring_hook<297>(p, one, st);
+    if (variant == 298) return launch_pring_hook<298>(p, one, st);
     if (variant == 202) return launch_pring<256, 128, 4, 2, 3>(p, one, 1, st);
     if (variant == 203) return launch_pring<128, 128, 2, 2, 3>(p, one, 1, st);
     if (variant == 204) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
