@@ -190,17 +190,17 @@ __global__ __launch_bounds__(NTH, 1) void conv1x1_rs_kernel(const ConvParams p, 
   });
   // stores into the void standing in for a previous unit's epilogue, so the first unit's counted waits
   // are the steady state's (distinct offsets: identical stores would be merged into one)
-  static_for<POOL ? 4 : 8>([&](auto kc) __attribute__((always_inline)) {
+  constexpr int NST = POOL ? 12 : 8;   // epilogue stores per unit
+  static_for<NST>([&](auto kc) __attribute__((always_inline)) {
     __builtin_amdgcn_raw_buffer_store_b128(u4{0u, 0u, 0u, 0u}, yr, 0x80000000u + decltype(kc)::value * 16, 0, 0);
   });
-  // one GEMM pass over the unit's K: 16 x 16 fragment MFMAs per k step for NM pixel rows, the next
-  // k step's 8 weight fragments read during this one's MFMAs; RECYCLE: each k step's X registers then
-  // take the next unit's (the fence keeps the loads there instead of letting the scheduler sink them
-  // below the pass's last MFMA)
-  auto pass = [&](auto nmc, auto recyc, int n0, f4 (&acc)[8][decltype(nmc)::value], auto&& operand, const Unit& nxt)
-      __attribute__((always_inline)) {
-    constexpr int NM = decltype(nmc)::value;
-    constexpr bool RECYCLE = decltype(recyc)::value;
+  // the pooled consumer's B operands, taken from X during the full pass (so X can be recycled there)
+  u4 pb[POOL ? KS : 1];
+  // the full pass over the unit's K: 16 fragment MFMAs per k step (8 weight fragments x 2 pixel rows),
+  // the next k step's weight fragments read during this one's MFMAs; then (POOL) this k step's 2x2 max,
+  // and the k step's X registers take the next unit's (the asm loads are ordered after the MFMAs that
+  // read them by their memory clobber)
+  auto full_pass = [&](int n0, f4 (&acc)[8][2], const Unit& nxt) __attribute__((always_inline)) {
     u4 wa[8], wb[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) wa[j] = wfrag(n0 + j * 16, 0);
@@ -212,31 +212,44 @@ __global__ __launch_bounds__(NTH, 1) void conv1x1_rs_kernel(const ConvParams p, 
 #pragma unroll
         for (int j = 0; j < 8; ++j) wn[j] = wfrag(n0 + j * 16, ks + 1);
       }
-      // this k step's X landed: the ops younger than its two loads are the rest of that unit's loads,
-      // the stores issued after them and (RECYCLE) this unit's loads so far — a constant per k step
-      if constexpr (!POOL) {
-        xwait<2 * KS + 6>(xs[0][ks], xs[1][ks]);
-      } else if (NM == 2) {
-        xwait<2 * (KS - 1 - ks) + 4>(xs[0][ks], xs[1][ks]);
-      }
-      u4 b[NM];
-      operand(ks, b);
+      // this k step's X landed: younger than its two loads are the rest of that unit's loads, the
+      // previous unit's epilogue stores and this unit's recycle loads so far — a constant
+      xwait<2 * KS - 2 + NST>(xs[0][ks], xs[1][ks]);
 #pragma unroll
       for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int r = 0; r < NM; ++r)
-          acc[j][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wc[j]), __builtin_bit_cast(h8, b[r]),
+        for (int r = 0; r < 2; ++r)
+          acc[j][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wc[j]), __builtin_bit_cast(h8, xs[r][ks]),
                                                              acc[j][r], 0, 0, 0);
-      if constexpr (RECYCLE) {
-        xs[0][ks] = load_xk(nxt, 0, std::integral_constant<int, ks>{});
-        xs[1][ks] = load_xk(nxt, 1, std::integral_constant<int, ks>{});
+      if constexpr (POOL) {
+        // 2x2 max: the two rows elementwise, then columns (li, li ^ 1) by quad-permute [1, 0, 3, 2];
+        // lanes with odd li compute a duplicate that is stored into the void
+        const u4 a0 = xs[0][ks], a1 = xs[1][ks];
+        pb[ks] = u4{pool2x2(a0.x, a1.x), pool2x2(a0.y, a1.y), pool2x2(a0.z, a1.z), pool2x2(a0.w, a1.w)};
       }
+      xs[0][ks] = load_xk(nxt, 0, std::integral_constant<int, ks>{});
+      xs[1][ks] = load_xk(nxt, 1, std::integral_constant<int, ks>{});
     });
   };
-  using I1 = std::integral_constant<int, 1>;
-  using I2 = std::integral_constant<int, 2>;
-  using T = std::true_type;
-  using F = std::false_type;
+  // the pooled consumer's pass: one pixel fragment per weight fragment
+  auto pooled_pass = [&](f4 (&acc)[8]) __attribute__((always_inline)) {
+    u4 wa[8], wb[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) wa[j] = wfrag(NF * 128 + j * 16, 0);
+    static_for<KS>([&](auto ksc) __attribute__((always_inline)) {
+      constexpr int ks = decltype(ksc)::value;
+      u4(&wc)[8] = (ks & 1) ? wb : wa;
+      u4(&wn)[8] = (ks & 1) ? wa : wb;
+      if (ks + 1 < KS) {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wn[j] = wfrag(NF * 128 + j * 16, ks + 1);
+      }
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wc[j]), __builtin_bit_cast(h8, pb[ks]), acc[j],
+                                                        0, 0, 0);
+    });
+  };
   for (int i = 0; i < ng; ++i) {
     wl = wl0;
     asm volatile("" : "+v"(wl));
@@ -249,31 +262,20 @@ __global__ __launch_bounds__(NTH, 1) void conv1x1_rs_kernel(const ConvParams p, 
         acc[j][0] = bv;
         acc[j][1] = bv;
       }
-      auto rows = [&](int ks, u4 (&b)[2]) __attribute__((always_inline)) {
-        b[0] = xs[0][ks];
-        b[1] = xs[1][ks];
-      };
-      if constexpr (POOL) pass(I2{}, F{}, cur.nh * 128, acc, rows, nxt);
-      else pass(I2{}, T{}, cur.nh * 128, acc, rows, nxt);
+      full_pass(cur.nh * 128, acc, nxt);
 #pragma unroll
       for (int r = 0; r < 2; ++r)
 #pragma unroll
         for (int m = 0; m < 4; ++m) store_pair(acc[2 * m][r], acc[2 * m + 1][r], yr, cur.yo + r * yrow + (uint32_t)(m * 64));
     }
     if constexpr (POOL) {
-      // the pooled consumer, after the full one's epilogue (its accumulators are free again): the 2x2
-      // max of each k step — the two rows elementwise, then columns (li, li ^ 1) by quad-permute
-      // [1, 0, 3, 2]; lanes with odd li compute a duplicate that is stored into the void
-      f4 acc[8][1];
+      // after the full consumer's epilogue (its accumulators are free again)
+      f4 acc[8];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) acc[j][0] = *reinterpret_cast<const f4*>(bias_l + NF * 128 + j * 16 + g * 4);
-      auto pooled = [&](int ks, u4 (&b)[1]) __attribute__((always_inline)) {
-        const u4 a0 = xs[0][ks], a1 = xs[1][ks];
-        b[0] = u4{pool2x2(a0.x, a1.x), pool2x2(a0.y, a1.y), pool2x2(a0.z, a1.z), pool2x2(a0.w, a1.w)};
-      };
-      pass(I1{}, T{}, NF * 128, acc, pooled, nxt);
+      for (int j = 0; j < 8; ++j) acc[j] = *reinterpret_cast<const f4*>(bias_l + NF * 128 + j * 16 + g * 4);
+      pooled_pass(acc);
 #pragma unroll
-      for (int m = 0; m < 4; ++m) store_pair(acc[2 * m][0], acc[2 * m + 1][0], y2r, cur.y2o + (uint32_t)(m * 64));
+      for (int m = 0; m < 4; ++m) store_pair(acc[2 * m], acc[2 * m + 1], y2r, cur.y2o + (uint32_t)(m * 64));
     }
     cur = nxt;
   }
