@@ -2203,8 +2203,10 @@ bool p8_default(const ConvParams& p) {
   static const int on = [] { const char* e = getenv("YV7_P8"); return e ? atoi(e) : 1; }();
   const bool one = p.k == 1 && p.s == 1 && p.pad == 0;
   const long t256 = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
+  // (1x1 K = 512 -> 512 @80, 1600 tiles: 167 -> 159 us in-network, profiles/r3u_tune.txt)
   return on && !p.pool && p.cout >= 256 && p.cout <= 1024 && p.cout % 8 == 0 && t256 >= 200 &&
-         ((one && p.K >= 1024) || (p.k == 3 && p.cin >= 256 && p.cin % BKE == 0));
+         ((one && p.K >= 1024) || (one && p.K >= 512 && p.cout >= 512 && t256 >= 1600) ||
+          (p.k == 3 && p.cin >= 256 && p.cin % BKE == 0));
 }
 
 // Stream-K form of the 8-phase ring (variant 237, or the dispatch with YV7_P8SK=1): the grid is every CU
