@@ -1135,12 +1135,21 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
   const int c = swz_bk<BK>(lr, lane % CPR);           // source chunk this lane fetches (slot = lane % CPR)
 
   const int nN = (p.cout + BN - 1) / BN;
-  const int T = ((p.M + BM - 1) / BM) * nN;
   const int nk = p.kpad / BK;
-  const TileWalk tw = xcd_tile_walk(T);   // XCD-major persistent tile order
+  // N-split weight-stationary form (WS with cout > BN): block b holds output-channel tile nb's weights
+  // and walks the M tiles only; the nN blocks of one virtual block share an XCD and walk the same M
+  // tiles in the same order, so each activation tile comes from HBM once and from that XCD's L2 for
+  // the other N tiles.  The launcher sizes the grid to a multiple of 8 nN.
+  const bool nsplit = WS != 0 && nN > 1;
+  const int nb = nsplit ? (int)((blockIdx.x / 8) % nN) : 0;
+  const int T = nsplit ? (p.M + BM - 1) / BM : ((p.M + BM - 1) / BM) * nN;
+  const TileWalk tw = nsplit ? xcd_tile_walk_g(T, gridDim.x / nN, (int)((blockIdx.x / (8 * nN)) * 8 + blockIdx.x % 8))
+                             : xcd_tile_walk(T);   // XCD-major persistent tile order
   const int ntl = tw.count();
   if (ntl == 0) return;
   const int nsteps = ntl * nk;
+  auto tile_m0 = [&](int t) { return nsplit ? t * BM : (t / nN) * BM; };
+  auto tile_n0 = [&](int t) { return nsplit ? nb * BN : (t % nN) * BN; };
 
   const auto xr = make_rsrc(p.x, p.xbytes);
   const auto wr = make_rsrc(p.w, p.wbytes);
@@ -1150,18 +1159,18 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
   if constexpr (WS == 0) {
     for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
   } else {
-    // (one N tile: cn0 = 0) this lane's channels, and the layer's weights into LDS once
+    // (one N tile per block: cn0 = nb * BN) this lane's channels, and the tile's weights into LDS once
 #pragma unroll
     for (int j = 0; j < TN; ++j)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const int col = wn * WTN + j * 16 + g * 4 + e;
+        const int col = nb * BN + wn * WTN + j * 16 + g * 4 + e;
         bias_r[j][e] = col < p.cout ? p.bias[col] : 0.0f;
       }
     constexpr int GPS = BN / RPI;   // DMA groups per K step
     for (int q = wave; q < nk * GPS; q += NW) {
       const int ks = q / GPS, rg = q - ks * GPS;
-      dma16(wr, wl + (ks * BN + rg * RPI) * RB_, (uint32_t)(((rg * RPI + lr) * p.kpad + c * 8) * 2),
+      dma16(wr, wl + (ks * BN + rg * RPI) * RB_, (uint32_t)(((nb * BN + rg * RPI + lr) * p.kpad + c * 8) * 2),
             (uint32_t)ks * BK * 2);
     }
   }
@@ -1173,7 +1182,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
   auto issue_next = [&]() __attribute__((always_inline)) {
     if (ikt == 0) {
       const int t = tw.at(it);
-      const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
+      const int m0 = tile_m0(t), n0 = tile_n0(t);
       aw.init(p, c, 0);
       PixelWalk pw(p, m0 + wave * RPI + lr);
 #pragma unroll
@@ -1203,8 +1212,8 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
   int cm0 = 0, cn0 = 0;
   auto init_tile = [&](int i) __attribute__((always_inline)) {
     const int t = tw.at(i);
-    cm0 = (t / nN) * BM;
-    cn0 = (t % nN) * BN;
+    cm0 = tile_m0(t);
+    cn0 = tile_n0(t);
 #pragma unroll
     for (int j = 0; j < TN; ++j) {
       const int col = cn0 + wn * WTN + j * 16 + g * 4;
@@ -2281,6 +2290,26 @@ hipError_t launch_pp(const ConvParams& p, int occ, hipStream_t st) {
   return hipGetLastError();
 }
 
+// the N-split weight-stationary 1x1 ring (cout > BN: block b holds N tile (b / 8) % nN; three stages)
+template <int BM, int BN, int WM, int WN, int KS>
+hipError_t launch_pring_wsn(const ConvParams& p, hipStream_t st) {
+  const int nN = (p.cout + BN - 1) / BN;
+  if (nN < 2 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || p.kpad > KS * 64 || p.k != 1 || p.s != 1 || p.pad)
+    return hipErrorInvalidValue;
+  const long T = (long)((p.M + BM - 1) / BM);
+  long per = device_cus() / nN / 8 * 8;   // virtual blocks per N tile, a multiple of 8
+  if (per > (T + 7) / 8 * 8) per = (T + 7) / 8 * 8;
+  if (per < 8) per = 8;
+  const int grid = (int)(per * nN);
+  if (p.act == 1)
+    YV7_LAUNCH((conv_f16_pring_kernel<BM, BN, WM, WN, 3, true, 1, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  else if (p.act == 2)
+    YV7_LAUNCH((conv_f16_pring_kernel<BM, BN, WM, WN, 3, true, 2, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  else
+    YV7_LAUNCH((conv_f16_pring_kernel<BM, BN, WM, WN, 3, true, 0, 64, KS>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
+  return hipGetLastError();
+}
+
 // the weight-stationary 1x1 ring (one N tile, whole K in LDS)
 template <int BM, int BN, int WM, int WN, int KS>
 hipError_t launch_pring_ws(const ConvParams& p, hipStream_t st) {
@@ -2475,8 +2504,11 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // @160 213 -> 201, @80 70 -> 66 / 66 -> 65; narrower or lower-resolution 1x1 layers lose.
     // YV7_WS1=0: off.
     static const int ws1 = [] { const char* e = getenv("YV7_WS1"); return e ? atoi(e) : 1; }();
+    // Round 3: its N-split form (two blocks per 256-pixel tile, each holding one 128-channel half of the
+    // weights, three activation stages in flight instead of two; tune_ops, us: 256->256 @160 197.6 ->
+    // 188.9, @80 60.3 -> 59.8 and 62.1 -> 58.6, profiles/r3w_tune.txt).
     if (ws1 && one && p.kpad <= 256 && p.cout > 128 && p.cout <= 256 && p.M >= 204800)
-      return launch_pring_ws<128, 256, 2, 4, 4>(p, st);
+      return launch_pring_wsn<256, 128, 4, 2, 4>(p, st);
     if (p8_default(p)) return launch_p8(p, one, st);
     if (one) {
       // (a cout that is not a multiple of 256 — the tensor-fused pair 512->256+128 @80 — would leave
@@ -2536,6 +2568,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 234 && one && p.cout <= 256 && p.kpad <= 256) return launch_pring_ws<128, 256, 2, 4, 4>(p, st);
     if (variant == 235 && one && p.cout <= 128 && p.kpad <= 256) return launch_pring_ws<256, 128, 4, 2, 4>(p, st);
     if (variant == 236 && one && p.cout <= 128 && p.kpad <= 512) return launch_pring_ws<128, 128, 2, 4, 8>(p, st);
+    // N-split weight-stationary 1x1 (K <= 256, 128 < cout <= 512): 256 x 128 tiles, three stages
+    if (variant == 239 && one && p.cout > 128 && p.cout <= 512 && p.kpad <= 256) return launch_pring_wsn<256, 128, 4, 2, 4>(p, st);
     if (variant == 232 && (one || p.cin % BKE == 0)) return launch_p8n(p, one, st);
     if (variant == 238 && p.cout <= 128 && (one || p.cin % BKE == 0)) return launch_p8w(p, one, st);
   }

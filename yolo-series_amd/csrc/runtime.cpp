@@ -362,7 +362,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (kind == YV7_OP_DETECT) return v == 92 || v == 97 || v == 99;
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
-  return (v >= 201 && v <= 206) || (v >= 211 && v <= 218) || (v >= 221 && v <= 223) || (v >= 231 && v <= 238) || v == 240 ||
+  return (v >= 201 && v <= 206) || (v >= 211 && v <= 218) || (v >= 221 && v <= 223) || (v >= 231 && v <= 240) ||
          (v >= 260 && v <= 262);
 }
 

@@ -73,6 +73,12 @@ __device__ __forceinline__ TileWalk xcd_tile_walk(int T) {
   return TileWalk{(int)((long)x * T / 8) + b / 8, gx, (int)((long)(x + 1) * T / 8)};
 }
 
+// The same walk for a block b of a virtual grid of G blocks (G a multiple of 8: b % 8 is its XCD).
+__device__ __forceinline__ TileWalk xcd_tile_walk_g(int T, int G, int b) {
+  const int x = b % 8, gx = G / 8;
+  return TileWalk{(int)((long)x * T / 8) + b / 8, gx, (int)((long)(x + 1) * T / 8)};
+}
+
 template <int ACT>
 __device__ __forceinline__ float act_t(float v) {
   // SiLU with v_exp_f32 / v_rcp_f32 (~1 ulp each): plenty for an fp16 output, ~4x cheaper than the
