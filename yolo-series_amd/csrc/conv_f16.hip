@@ -2535,6 +2535,13 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // 188.9, @80 60.3 -> 59.8 and 62.1 -> 58.6, profiles/r3w_tune.txt).
     if (ws1 && one && p.kpad <= 256 && p.cout > 128 && p.cout <= 256 && p.M >= 204800)
       return launch_pring_wsn<256, 128, 4, 2, 4>(p, st);
+    // 3x3 stride-2 layers with about one round of 256 x 128 tiles: the 8-phase ring on 256 x 128 tiles
+    // (all-layer sweep, profiles/r3y_tune.txt, us: 512->512 s2 @40 81.9 -> 75.5, 128->128 s2 @80
+    // 29.6 -> 26.5)
+    if (p.k == 3 && p.s == 2 && p.cin >= 128 && p.cin % BKE == 0 && p.cout % 128 == 0 && p.cout <= 1024) {
+      const long t2n = (long)((p.M + 255) / 256) * (p.cout / 128);
+      if (t2n >= 150 && t2n <= 250) return launch_p8n(p, false, st);
+    }
     if (p8_default(p)) return launch_p8(p, one, st);
     if (one) {
       // (a cout that is not a multiple of 256 — the tensor-fused pair 512->256+128 @80 — would leave
