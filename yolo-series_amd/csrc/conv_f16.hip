@@ -539,38 +539,8 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
   // the level's anchors once (a per-lane kernel-argument load: its wait stays out of the tile loop)
   if (tid < 8) det_tab_ptrs<BM, BN>(es).anc[tid] = p.anchor[tid];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  // the previous tile's sigmoid staging into zs (z's layout); the 4 box columns of each row are decoded
-  // in det_tail_fixed (one (row, column) per thread there, beside the row scores)
-  auto staging = [&](const f4 (&a)[TN][TM]) __attribute__((always_inline)) {
-    if constexpr (HOOK != 1) {
-      float* zs = reinterpret_cast<float*>(es);
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int roff = (wm * WTM + i * 16 + li) * NO;
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) zs[zo[j][e] + (zo[j][e] < NA * BM * NO ? roff : 0)] = det_sig(a[j][i][e]);
-      }
-    }
-  };
-  auto tail = [&](int m0) __attribute__((always_inline)) {
-    // z / record rows of the tile relative to its first pixel's row (offsets stay 32-bit at any batch)
-    const int mb = m0 / hw;
-    const long long zb = (long long)mb * p.nrows + p.row_off + (m0 - mb * hw);
-    const auto zr = make_rsrc(p.z + (size_t)zb * 85, 0x7fffffffu);
-    const auto br = make_rsrc(p.best ? p.best + (size_t)zb * 4 : p.z, 0x7fffffffu);
-    det_tail_fixed<BM, NTH>(p, es, tid, zr, br, zb);
-  };
-  // Tile t's epilogue is software-pipelined into tile t + 1: its accumulators are kept (pacc), their
-  // sigmoid staging and its row table are written in tile t + 1's first K step (behind that step's
-  // barrier: every wave's tail of tile t - 1 has read zs / the table by then), and its tail (row scores,
-  // box decode, z and record stores) runs after tile t + 1's K loop.  The sigmoid (~21 us of the 80^2
-  // head, profiles/r3m_det_ab.txt hook 98) then overlaps the MFMAs instead of stalling both SIMD waves.
   issue();
   issue();
-  f4 pacc[TN][TM];
-  int pm0 = 0;
   for (int it = 0; it < ntl; ++it) {
     const int m0 = tw.at(it) * BM;
     f4 acc[TN][TM];
@@ -579,14 +549,13 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[j][i] = bv[j];
     for (int k = 0; k < nk; ++k) {
-      // stage (it, k) landed: younger are stage (it, 1) and the stores of the tail run in the previous
-      // iteration (the tail of tile it - 2) at k = 0, those stores at k = 1 (both stages of a tile
-      // start are issued before them)
+      // stage (it, k) landed: younger are stage (it, 1) and the previous epilogue's stores at k = 0,
+      // the previous epilogue's stores at k = 1 (both stages of a tile start are issued before them)
       if (k == 0) {
-        if (it > 1 && nst == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 10) : "memory");
-        else if (it > 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 8) : "memory");
+        if (it > 0 && nst == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 10) : "memory");
+        else if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 8) : "memory");
         else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-      } else if (k == 1 && it > 1) {
+      } else if (k == 1 && it > 0) {
         if (nst == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
         else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       } else {
@@ -594,7 +563,7 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
       }
       __builtin_amdgcn_s_barrier();
       if (k >= 1) issue();              // stage (it, k + 1) or the next tile's first stage
-      if (k == 0 && it > 0) det_table<BM, BN, NTH, false>(p, es, pm0, tid);   // the previous tile's rows
+      if (k == 0) det_table<BM, BN, NTH, false>(p, es, m0, tid);   // read after the K loop's last barrier
       const unsigned char* As = smem + ((it * nk + k) & 1) * STAGE;
       const unsigned char* Bs = As + BM * ROWB;
 #pragma unroll
@@ -619,29 +588,34 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]),
                                                                __builtin_bit_cast(h8, xa[i]), acc[j][i], 0, 0, 0);
         __builtin_amdgcn_s_setprio(0);
-        // the previous tile's staging beside this step's first MFMA cluster
-        if (s == 0 && k == 0 && it > 0) staging(pacc);
       }
     }
-    // ring reads and the previous tile's staging done -> the next tile's stage (it + 1, 1) into the
-    // free slot, then the previous tile's tail
+    // epilogue: ring reads done -> the next tile's stage (it + 1, 1) into the free slot
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     issue();
-    if (it > 0) tail(pm0);
+    if constexpr (HOOK != 1) {
+      // staging: the sigmoid of every logit into zs (z's layout); the 4 box columns of each row are
+      // decoded in det_tail_fixed (one (row, column) per thread there, beside the row scores)
+      float* zs = reinterpret_cast<float*>(es);
 #pragma unroll
-    for (int j = 0; j < TN; ++j)
+      for (int i = 0; i < TM; ++i) {
+        const int roff = (wm * WTM + i * 16 + li) * NO;
 #pragma unroll
-      for (int i = 0; i < TM; ++i) pacc[j][i] = acc[j][i];
-    pm0 = m0;
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) zs[zo[j][e] + (zo[j][e] < NA * BM * NO ? roff : 0)] = det_sig(acc[j][i][e]);
+      }
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // z / record rows of this tile relative to its first pixel's row (offsets stay 32-bit at any batch)
+    const int mb = m0 / hw;
+    const long long zb = (long long)mb * p.nrows + p.row_off + (m0 - mb * hw);
+    const auto zr = make_rsrc(p.z + (size_t)zb * 85, 0x7fffffffu);
+    const auto br = make_rsrc(p.best ? p.best + (size_t)zb * 4 : p.z, 0x7fffffffu);
+    det_tail_fixed<BM, NTH>(p, es, tid, zr, br, zb);
   }
-  // the last tile: its table and staging behind a barrier (every wave's last tail read zs first), tail
-  __builtin_amdgcn_s_barrier();
-  det_table<BM, BN, NTH, false>(p, es, pm0, tid);
-  staging(pacc);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  tail(pm0);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
