@@ -1,0 +1,59 @@
+#!/bin/bash
+# One GPU call as a chain of steps (the round's A/B drivers), each under its own time limit; the chain
+# stops at the first failing step.  Outputs land in gpurun_out/TAG/.
+#
+# usage: bash scripts/gpu_steps.sh TAG STEP [STEP ...]
+#   tests[=PYTEST_PATHS]        GPU suite (default: tests), -x, per-test timeout       -> tests.log
+#   smoke                       __graft_entry__.smoke()                                -> smoke.log
+#   ops[=NAME][@ENV=V,ENV=V]    serial per-op profile (scripts/op_profile.py) under the env
+#                                                                                     -> ops_NAME.txt
+#   tune=OPS:CANDS[:ROUNDS]     tune_ops.py: each candidate forced on one op at a time -> tune.txt
+#                               (OPS = all for every conv op)
+#   bench[=N][@ENV=V,...]       N bench lines (default 2), --steps 40 --warmup 5       -> bench_I.json
+# e.g. bash scripts/gpu_steps.sh r4a tests ops=base ops=nodual@YV7_DUAL=0 tune=8,12:239,234:3 bench=2
+set -o pipefail
+R=$GRAFT_REPO_ROOT
+TAG=$1; shift
+O=gpurun_out/$TAG
+cd $R && mkdir -p $O
+export PYTHONPATH=$R/yolo-series_amd:$R
+
+envof() {   # "A=1,B=2" -> "A=1 B=2"
+  [ -n "$1" ] && echo "${1//,/ }"
+}
+
+for step in "$@"; do
+  name=${step%%=*}; arg=; [ "$step" != "$name" ] && arg=${step#*=}
+  envs=; case "$arg" in *@*) envs=${arg#*@}; arg=${arg%%@*};; esac
+  case "$name" in *@*) envs=${name#*@}; name=${name%%@*};; esac
+  echo "== $step"
+  case "$name" in
+    tests)
+      timeout -k 10 600 python -u -m pytest ${arg:-tests} -m gpu -x -v --timeout 300 --timeout-method thread -rf \
+        > $O/tests.log 2>&1
+      rc=$?; grep -E "passed|failed" $O/tests.log | tail -1; grep -E "^FAILED" $O/tests.log | head
+      [ $rc -eq 0 ] || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 \
+        || { cat $O/smoke.log; exit 1; }
+      tail -1 $O/smoke.log ;;
+    ops)
+      f=$O/ops_${arg:-base}.txt
+      env $(envof "$envs") timeout -k 10 300 python -u scripts/op_profile.py --top 100 > $f 2>&1 || { tail $f; exit 1; }
+      grep -E "^forward" $f ;;
+    tune)
+      IFS=: read -r ops cands rounds <<< "$arg"
+      sel="--ops $ops"; [ "$ops" = all ] && sel=
+      timeout -k 10 1100 python -u scripts/tune_ops.py $sel --cands $cands --rounds ${rounds:-2} \
+        > $O/tune.txt 2>&1 || { tail -20 $O/tune.txt; exit 1; }
+      grep -v amdgpu.ids $O/tune.txt | tail -90 ;;
+    bench)
+      for r in $(seq 1 ${arg:-2}); do
+        f=$O/bench_${envs:+${envs//[=,]/_}_}$r.json
+        env $(envof "$envs") timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --no-cpu-baseline \
+          > $f 2> ${f%.json}.err || exit 1
+        python -c "import json;d=json.load(open('$f'));print('bench', '$envs', d['value'], d['detail']['serial_forward_ms'])"
+      done ;;
+    *) echo "unknown step $step"; exit 2 ;;
+  esac
+done
