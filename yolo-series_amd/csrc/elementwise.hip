@@ -90,18 +90,25 @@ __global__ __launch_bounds__(NT) void maxpool_kernel(const T* __restrict__ x, in
   }
 }
 
+// one thread per input pixel and 16-byte chunk: one load, the 2 x 2 output block's four stores (a
+// quarter of the index arithmetic of one thread per output)
 template <typename T>
 __global__ __launch_bounds__(NT) void upsample_kernel(const T* __restrict__ x, int B, int H, int W, int xc, int xoff,
                                                       T* __restrict__ y, int yc, int yoff, int C) {
   constexpr int V = Vec<T>::N;
   const int cv = C / V, Ho = 2 * H, Wo = 2 * W;
-  const int total = B * Ho * Wo * cv;
+  const int total = B * H * W * cv;
+  const size_t yrow = (size_t)(Wo + 2 * BORDER) * yc;   // elements per output row
   for (int i = blockIdx.x * NT + threadIdx.x; i < total; i += gridDim.x * NT) {
     const int pix = i / cv, c = (i - pix * cv) * V;
-    const int t = pix / Wo, wo = pix - t * Wo;
-    const int b = t / Ho, ho = t - b * Ho;
-    *reinterpret_cast<u4*>(y + pix_index(b, ho, wo, Ho, Wo) * yc + yoff + c) =
-        *reinterpret_cast<const u4*>(x + pix_index(b, ho >> 1, wo >> 1, H, W) * xc + xoff + c);
+    const int t = pix / W, w = pix - t * W;
+    const int b = t / H, h = t - b * H;
+    const u4 v = *reinterpret_cast<const u4*>(x + pix_index(b, h, w, H, W) * xc + xoff + c);
+    T* o = y + pix_index(b, 2 * h, 2 * w, Ho, Wo) * yc + yoff + c;
+    *reinterpret_cast<u4*>(o) = v;
+    *reinterpret_cast<u4*>(o + yc) = v;
+    *reinterpret_cast<u4*>(o + yrow) = v;
+    *reinterpret_cast<u4*>(o + yrow + yc) = v;
   }
 }
 
@@ -286,7 +293,7 @@ hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc,
 
 hipError_t launch_upsample2x(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int yc, int yoff,
                              int C, hipStream_t st) {
-  const size_t work = (size_t)B * 4 * H * W * (C / (dtype == 1 ? 8 : 4));
+  const size_t work = (size_t)B * H * W * (C / (dtype == 1 ? 8 : 4));
   if (dtype == 1)
     YV7_LAUNCH(upsample_kernel<_Float16>, dim3(grid_for(work)), dim3(NT), 0, st, (const _Float16*)x, B, H, W,
                        xc, xoff, (_Float16*)y, yc, yoff, C);
