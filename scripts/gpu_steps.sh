@@ -9,8 +9,11 @@
 #                                                                                     -> ops_NAME.txt
 #   tune=OPS:CANDS[:ROUNDS]     tune_ops.py: each candidate forced on one op at a time -> tune.txt
 #                               (OPS = all for every conv op)
-#   bench[=N][@ENV=V,...]       N bench lines (default 2), --steps 40 --warmup 5       -> bench_I.json
+#   bench[=N][@ENV=V,...]       N bench lines (default 2), --steps 40 --warmup 5  -> bench_STEP_I.json
+#   lib=NAME                    run the following steps on yolo-series_amd/yv7/libyv7_NAME.so (an
+#                               A/B baseline built elsewhere); lib=cur restores the tree's library
 # e.g. bash scripts/gpu_steps.sh r4a tests ops=base ops=nodual@YV7_DUAL=0 tune=8,12:239,234:3 bench=2
+#      bash scripts/gpu_steps.sh r4b ops=new lib=base ops=old lib=cur bench=1 lib=base bench=1 lib=cur
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=$1; shift
@@ -22,7 +25,10 @@ envof() {   # "A=1,B=2" -> "A=1 B=2"
   [ -n "$1" ] && echo "${1//,/ }"
 }
 
+LIBD=$R/yolo-series_amd/yv7
+n=0
 for step in "$@"; do
+  n=$((n + 1))
   name=${step%%=*}; arg=; [ "$step" != "$name" ] && arg=${step#*=}
   envs=; case "$arg" in *@*) envs=${arg#*@}; arg=${arg%%@*};; esac
   case "$name" in *@*) envs=${name#*@}; name=${name%%@*};; esac
@@ -49,11 +55,14 @@ for step in "$@"; do
       grep -v amdgpu.ids $O/tune.txt | tail -90 ;;
     bench)
       for r in $(seq 1 ${arg:-2}); do
-        f=$O/bench_${envs:+${envs//[=,]/_}_}$r.json
+        f=$O/bench_${n}_$r.json
         env $(envof "$envs") timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --no-cpu-baseline \
           > $f 2> ${f%.json}.err || exit 1
-        python -c "import json;d=json.load(open('$f'));print('bench', '$envs', d['value'], d['detail']['serial_forward_ms'])"
+        python -c "import json;d=json.load(open('$f'));print('bench', '$f', '$envs', d['value'], d['detail']['serial_forward_ms'])"
       done ;;
+    lib)
+      [ -f $LIBD/libyv7_cur.so ] || cp $LIBD/libyv7.so $LIBD/libyv7_cur.so
+      cp $LIBD/libyv7_$arg.so $LIBD/libyv7.so || exit 1 ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
 done

@@ -83,18 +83,32 @@ __global__ __launch_bounds__(NTH, 1) void conv1x1_rs_kernel(const ConvParams p, 
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int g = lane >> 4, li = lane & 15;
 
-  // weights -> LDS once: row n (full consumer's channels, then the pooled consumer's), 16-byte chunks
+  // weights -> LDS once: row n (full consumer's channels, then the pooled consumer's), 16-byte chunks;
+  // every load of a thread is issued before its first LDS write (a loop of load -> write pairs waited
+  // out one L2 / HBM round trip per chunk: 8-16 in a row, ~20 us of the 80^2 launch)
   {
     const unsigned char* w1 = reinterpret_cast<const unsigned char*>(p.w);
     const unsigned char* w2 = reinterpret_cast<const unsigned char*>(q.w);
     constexpr int CH = K / 8;   // 16-byte chunks per row
-    for (int i = tid; i < NROWS * CH; i += NTH) {
-      const int n = i / CH, c = i - n * CH;
+    constexpr int IT = NROWS * CH / NTH;
+    static_assert(NROWS * CH % NTH == 0, "whole chunks per thread");
+    u4 wv[IT];
+#pragma unroll
+    for (int t = 0; t < IT; ++t) {
+      const int i = tid + t * NTH, n = i / CH, c = i - n * CH;
       const unsigned char* src = n < NF * 128 ? w1 + ((size_t)n * p.kpad + c * 8) * 2
                                               : w2 + ((size_t)(n - NF * 128) * p.kpad + c * 8) * 2;
-      *reinterpret_cast<u4*>(smem + n * ROW + c * 16) = *reinterpret_cast<const u4*>(src);
+      wv[t] = *reinterpret_cast<const u4*>(src);
     }
-    for (int n = tid; n < NROWS; n += NTH) bias_l[n] = n < NF * 128 ? p.bias[n] : q.bias[n - NF * 128];
+    float bv = 0.f;
+    if (tid < NROWS) bv = tid < NF * 128 ? p.bias[tid] : q.bias[tid - NF * 128];
+#pragma unroll
+    for (int t = 0; t < IT; ++t) {
+      const int i = tid + t * NTH, n = i / CH, c = i - n * CH;
+      *reinterpret_cast<u4*>(smem + n * ROW + c * 16) = wv[t];
+    }
+    static_assert(NROWS <= NTH, "one bias per thread");
+    if (tid < NROWS) bias_l[tid] = bv;
   }
   __syncthreads();
 

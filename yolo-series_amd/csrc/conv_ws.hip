@@ -53,6 +53,32 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint3
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, vo, so, 0, 0);
 }
 
+// The layer's weights -> LDS once per block: tap t, out channel n, 16-byte slot s holds K chunk
+// s ^ (n & 7) of that tap.  A thread's 18 chunks go as two batches of 9 loads issued before their LDS
+// writes (as a load -> write loop, hipcc waited out one L2 round trip per chunk: 18 in a row before
+// the first patch DMA of every block).
+__device__ __forceinline__ void load_weights(const ConvParams& p, unsigned char* wl, int tid) {
+  constexpr int NQ = 9 * CO * 8, IT = NQ / NT, NB = 9;
+  static_assert(NQ % NT == 0 && IT % NB == 0, "whole batches of chunks per thread");
+  const unsigned char* w = reinterpret_cast<const unsigned char*>(p.w);
+#pragma unroll
+  for (int b0 = 0; b0 < IT; b0 += NB) {
+    u4 v[NB];
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int q = tid + (b0 + j) * NT;
+      const int t = q / (CO * 8), rem = q - t * CO * 8, n = rem >> 3, slot = rem & 7;
+      v[j] = *reinterpret_cast<const u4*>(w + ((size_t)n * p.kpad + t * CI + (slot ^ (n & 7)) * 8) * 2);
+    }
+#pragma unroll
+    for (int j = 0; j < NB; ++j) {
+      const int q = tid + (b0 + j) * NT;
+      const int t = q / (CO * 8), rem = q - t * CO * 8, n = rem >> 3, slot = rem & 7;
+      *reinterpret_cast<u4*>(wl + t * WTAP + n * 128 + slot * 16) = v[j];
+    }
+  }
+}
+
 // HOOK: microbenchmark builds only (scripts/convbench.hip; the ABI never accepts them) — 12 no output
 // stores, 13 no patch DMA, 14 no epilogue, 16 MFMA loop only.  Compile-time, so that the production
 // form has no runtime test between the MFMAs and the previous tile's epilogue: a branch there puts the
@@ -79,15 +105,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     for (int e = 0; e < 4; ++e) bias[j][e] = p.bias[j * 16 + g * 4 + e];
 
   // weights -> LDS once: tap t, out channel n, 16-byte slot s holds K chunk s ^ (n & 7) of that tap
-  {
-    const unsigned char* w = reinterpret_cast<const unsigned char*>(p.w);
-    for (int q = tid; q < 9 * CO * 8; q += NT) {
-      const int t = q / (CO * 8), rem = q - t * CO * 8, n = rem >> 3, slot = rem & 7;
-      const int chunk = slot ^ (n & 7);
-      const u4 v = *reinterpret_cast<const u4*>(w + ((size_t)n * p.kpad + t * CI + chunk * 8) * 2);
-      *reinterpret_cast<u4*>(wl + t * WTAP + n * 128 + slot * 16) = v;
-    }
-  }
+  load_weights(p, wl, tid);
 
   // patch DMA: wave w moves groups w, w+4, ... (waves 1-3 repeat their last group so that every wave
   // issues GPW instructions: identical bytes to the same LDS addresses).  Lane l of group G: patch
@@ -351,15 +369,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64r_kernel(const ConvParams p
   if (tid < CO) bias_l[tid] = p.bias[tid];
 
   // weights -> LDS once (the layout of the kernel above)
-  {
-    const unsigned char* w = reinterpret_cast<const unsigned char*>(p.w);
-    for (int q = tid; q < 9 * CO * 8; q += NT) {
-      const int t = q / (CO * 8), rem = q - t * CO * 8, n = rem >> 3, slot = rem & 7;
-      const int chunk = slot ^ (n & 7);
-      const u4 v = *reinterpret_cast<const u4*>(w + ((size_t)n * p.kpad + t * CI + chunk * 8) * 2);
-      *reinterpret_cast<u4*>(wl + t * WTAP + n * 128 + slot * 16) = v;
-    }
-  }
+  load_weights(p, wl, tid);
 
   // half-patch DMA: piece G = wave + 4k (k < 5), the sixth is piece 20 for every wave.  Lane l of piece
   // G: patch pixel pp = 16 G + (l >> 2), LDS slot l & 3 of its 64-B row holds source chunk
