@@ -134,13 +134,8 @@ __global__ __launch_bounds__(NT) void copy_kernel(const T* __restrict__ x, int B
 //      staged in LDS once; each 5 x 5 pool runs separably (a 5-wide row max into a scratch plane, then
 //      a 5-tall column max: 10 LDS reads per output instead of 25; taps outside the image re-read the
 //      centre, max being idempotent = the -inf padding), ping-ponging between two planes; every
-//      stage's output also leaves as 16-byte stores into its concat slice.  A thread's items (pixel,
-//      16-byte chunk) and their coordinates are computed once and kept in registers for the load, the
-//      six passes and the stores: the per-pass index arithmetic (divisions by W) was most of the
-//      kernel's instructions at 20^2.
+//      stage's output also leaves as 16-byte stores into its concat slice.
 constexpr int SPP_CG = 16;
-constexpr int SPP_LDS = 64 * 1024;                    // three planes
-constexpr int SPP_MAXI = (SPP_LDS / 3 / 16 + NT - 1) / NT;   // items per thread at most
 
 template <typename T>
 __global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x, int B, int H, int W, int xc,
@@ -155,16 +150,9 @@ __global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x
   u4* buf0 = reinterpret_cast<u4*>(lds);
   u4* buf1 = buf0 + items;
   u4* tmp = buf1 + items;
-  int hh[SPP_MAXI], ww[SPP_MAXI];
-  size_t go[SPP_MAXI];   // element offset of the item's 16 bytes in x (channel slice coff + c0 + chunk)
-#pragma unroll
-  for (int k = 0; k < SPP_MAXI; ++k) {
-    const int i = k * NT + threadIdx.x;
+  for (int i = threadIdx.x; i < items; i += NT) {
     const int px = i / NCH, ch = i - px * NCH, h = px / W, w = px - h * W;
-    hh[k] = h;
-    ww[k] = w;
-    go[k] = i < items ? pix_index(b, h, w, H, W) * xc + coff + c0 + ch * V : 0;
-    if (i < items) buf0[i] = *reinterpret_cast<const u4*>(x + go[k]);
+    buf0[i] = *reinterpret_cast<const u4*>(x + pix_index(b, h, w, H, W) * xc + coff + c0 + ch * V);
   }
   __syncthreads();
   auto vmax = [](u4 a, u4 c) -> u4 {
@@ -179,35 +167,29 @@ __global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x
   u4* src = buf0;
   u4* dst = buf1;
   for (int stage = 1; stage <= 3; ++stage) {
+    for (int i = threadIdx.x; i < items; i += NT) {   // row max: 5 taps along w
+      const int px = i / NCH, ch = i - px * NCH, w = px % W;
+      u4 m = src[i];
 #pragma unroll
-    for (int k = 0; k < SPP_MAXI; ++k) {   // row max: 5 taps along w
-      const int i = k * NT + threadIdx.x;
-      if (i < items) {
-        u4 m = src[i];
-#pragma unroll
-        for (int dx = -2; dx <= 2; ++dx) {
-          if (dx == 0) continue;
-          const bool in = (unsigned)(ww[k] + dx) < (unsigned)W;
-          m = vmax(m, src[in ? i + dx * NCH : i]);
-        }
-        tmp[i] = m;
+      for (int dx = -2; dx <= 2; ++dx) {
+        if (dx == 0) continue;
+        const bool in = (unsigned)(w + dx) < (unsigned)W;
+        m = vmax(m, src[(in ? px + dx : px) * NCH + ch]);
       }
+      tmp[i] = m;
     }
     __syncthreads();
+    for (int i = threadIdx.x; i < items; i += NT) {   // column max: 5 taps along h
+      const int px = i / NCH, ch = i - px * NCH, h = px / W, w = px - h * W;
+      u4 m = tmp[i];
 #pragma unroll
-    for (int k = 0; k < SPP_MAXI; ++k) {   // column max: 5 taps along h
-      const int i = k * NT + threadIdx.x;
-      if (i < items) {
-        u4 m = tmp[i];
-#pragma unroll
-        for (int dy = -2; dy <= 2; ++dy) {
-          if (dy == 0) continue;
-          const bool in = (unsigned)(hh[k] + dy) < (unsigned)H;
-          m = vmax(m, tmp[in ? i + dy * W * NCH : i]);
-        }
-        dst[i] = m;
-        *reinterpret_cast<u4*>(y + go[k] + stage * C) = m;
+      for (int dy = -2; dy <= 2; ++dy) {
+        if (dy == 0) continue;
+        const bool in = (unsigned)(h + dy) < (unsigned)H;
+        m = vmax(m, tmp[(in ? px + dy * W : px) * NCH + ch]);
       }
+      dst[i] = m;
+      *reinterpret_cast<u4*>(y + pix_index(b, h, w, H, W) * xc + coff + stage * C + c0 + ch * V) = m;
     }
     __syncthreads();
     u4* t = src;
@@ -317,7 +299,7 @@ hipError_t launch_copy(int dtype, const void* x, int B, int H, int W, int xc, in
 
 bool spp_cascade_supported(int dtype, int H, int W, int C) {
   const int V = dtype == 1 ? 8 : 4;
-  return C % SPP_CG == 0 && (size_t)3 * H * W * (SPP_CG / V) * 16 <= SPP_LDS;
+  return C % SPP_CG == 0 && (size_t)3 * H * W * (SPP_CG / V) * 16 <= 64 * 1024;
 }
 
 // x: the concat tensor (pitch xc) holding the pool input at channel slice [coff, coff + C); the three
