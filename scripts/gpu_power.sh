@@ -3,12 +3,12 @@
 # rocm-smi sampled every ~0.5 s beside `bench.py --steps 1500`, plus an idle sample before.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-TAG=${1:-r3pw}
+TAG=${1:-r3pw}; shift; EXTRA="$@"   # extra bench.py arguments, e.g. --streams 1
 O=gpurun_out/$TAG
 cd $R && mkdir -p $O
 export PYTHONPATH=$R/yolo-series_amd:$R
 timeout -k 5 20 rocm-smi --showpower --showclocks --showtemp > $O/idle.txt 2>&1
-timeout -k 10 300 python -u bench.py --steps 1500 --warmup 20 --no-cpu-baseline > $O/bench.json 2> $O/bench.err &
+timeout -k 10 300 python -u bench.py --steps 1500 --warmup 20 --no-cpu-baseline $EXTRA > $O/bench.json 2> $O/bench.err &
 BP=$!
 for i in $(seq 1 60); do
   kill -0 $BP 2>/dev/null || break
