@@ -28,8 +28,8 @@ constexpr int C = 256, CM = 256, CO = 128, NTH = 512;
 constexpr int WROW = CM * 2;                       // bytes per resident weight row (256 k)
 constexpr int W2OFF = 0, W3OFF = CO * WROW, W1OFF = 2 * CO * WROW;
 constexpr int W1CH = 16 * C * 2;                   // one W1 chunk: 16 rows x 256 k = 8 KiB
-constexpr int BOFF = W1OFF + 2 * W1CH;
-constexpr int LDS = BOFF + (CM + 2 * CO) * 4;      // 148,480 B
+constexpr int BOFF = W1OFF + 3 * W1CH;         // W1 ring: 2 buffers (register-staged) or 3 (DMA)
+constexpr int LDS = BOFF + (CM + 2 * CO) * 4;      // 156,672 B
 
 __device__ __forceinline__ float silu(float v) {
   return v * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(-1.4426950408889634f * v));
@@ -46,6 +46,7 @@ __device__ __forceinline__ uint32_t pool2x2(uint32_t r0, uint32_t r1) {
 }
 
 // x [B][H][W][256], W1 [256][256], W2p / W3p [128][256] (k permuted), y2 [B][H][W][128], y3 [B][H/2][W/2][128]
+template <bool DMA>
 __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restrict__ x, const _Float16* __restrict__ W1,
                                                       const float* __restrict__ b1, const _Float16* __restrict__ W2p,
                                                       const float* __restrict__ b2, const _Float16* __restrict__ W3p,
@@ -76,8 +77,24 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
   const int w1r = tid >> 5, w1q = tid & 31;
   auto w1load = [&](int c) { return *reinterpret_cast<const u4*>(W1 + (c * 16 + w1r) * C + w1q * 8); };
   auto w1store = [&](int buf, u4 v) { *reinterpret_cast<u4*>(smem + W1OFF + buf * W1CH + slot(w1r, w1q)) = v; };
-  w1store(0, w1load(0));
+  // DMA form: wave w's lane l moves row 2 w + l / 32, LDS slot l % 32 of a chunk, i.e. source chunk
+  // (l % 32) ^ (row & 15) — the swizzle applied on the source side (the DMA writes 16 B per lane in lane order)
+  const auto w1rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(W1), (short)0, CM * C * 2, 0x00020000);
+  const int dr = 2 * wave + (lane >> 5), dq = (lane & 31) ^ (dr & 15);
+  auto w1dma = [&](int c, int b) __attribute__((always_inline)) {
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(
+        w1rs, (__attribute__((address_space(3))) void*)(smem + W1OFF + b * W1CH + wave * 1024), 16,
+        (uint32_t)(((c * 16 + dr) * C + dq * 8) * 2), 0, 0, 0);
+  };
+  if constexpr (DMA) {
+    w1dma(0, 0);
+    w1dma(1, 1);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    w1store(0, w1load(0));
+  }
   __syncthreads();
+  int n = 0;   // W1 chunk sequence number (DMA ring position n % 3)
 
   const int segs = W / 16, rps = H / 2;
   const int U = B * rps * segs;
@@ -107,8 +124,10 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
     // one W1 chunk: y1 rows 16 c .. +15 for both pixel rows; the next chunk's load in flight meanwhile,
     // then its LDS write and the block barrier
     auto chunk = [&](int c, f4 (&a1)[2]) __attribute__((always_inline)) {
-      const u4 nxt = w1load((c + 1) & 15);      // the next chunk (the next unit's chunk 0 after c = 15)
-      const unsigned char* w1b = smem + W1OFF + buf * W1CH;
+      u4 nxt;
+      if constexpr (DMA) w1dma((c + 2) & 15, (n + 2) % 3);   // two chunks ahead into the buffer read at n - 1
+      else nxt = w1load((c + 1) & 15);      // the next chunk (the next unit's chunk 0 after c = 15)
+      const unsigned char* w1b = smem + W1OFF + (DMA ? n % 3 : buf) * W1CH;
       const f4 bv1 = *reinterpret_cast<const f4*>(bl + c * 16 + g * 4);
       a1[0] = bv1;
       a1[1] = bv1;
@@ -119,9 +138,17 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
         for (int r = 0; r < 2; ++r)
           a1[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wf), __builtin_bit_cast(h8, xs[r][ks]), a1[r], 0, 0, 0);
       }
-      w1store(buf ^ 1, nxt);
-      __syncthreads();
-      buf ^= 1;
+      if constexpr (DMA) {
+        // chunk n + 1 (issued one step ago) has landed: younger VMEM ops are chunk n + 2's DMA only
+        // (or, at a unit's first step, also this unit's X loads and the last unit's stores: waited too)
+        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        __builtin_amdgcn_s_barrier();   // raw: __syncthreads' fence would drain chunk n + 2's DMA too
+        ++n;
+      } else {
+        w1store(buf ^ 1, nxt);
+        __syncthreads();
+        buf ^= 1;
+      }
     };
 #pragma unroll 1
     for (int s2 = 0; s2 < 8; ++s2) {
@@ -175,6 +202,7 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
       }
     }
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the ring's last DMAs (into the void of the next unit)
 }
 
 int main(int argc, char** argv) {
@@ -217,13 +245,20 @@ int main(int argc, char** argv) {
   int cus = 256;
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const int grid = cus;
-  chain_kernel<<<grid, NTH>>>(dx, dW1, db1, dW2p, db2, dW3p, db3, dy2, dy3, B, H, W);
+  const bool dma = argc > 2 && argv[2][0] == 'd';
+  auto launch = [&] {
+    if (dma) chain_kernel<true><<<grid, NTH>>>(dx, dW1, db1, dW2p, db2, dW3p, db3, dy2, dy3, B, H, W);
+    else chain_kernel<false><<<grid, NTH>>>(dx, dW1, db1, dW2p, db2, dW3p, db3, dy2, dy3, B, H, W);
+  };
+  (void)hipMemset(dy2, 0, ny2 * 2);
+  (void)hipMemset(dy3, 0, ny3 * 2);
+  launch();
   if (hipDeviceSynchronize() != hipSuccess) return 3;
   hipEvent_t e0, e1;
   (void)hipEventCreate(&e0);
   (void)hipEventCreate(&e1);
   (void)hipEventRecord(e0);
-  for (int i = 0; i < iters; ++i) chain_kernel<<<grid, NTH>>>(dx, dW1, db1, dW2p, db2, dW3p, db3, dy2, dy3, B, H, W);
+  for (int i = 0; i < iters; ++i) launch();
   (void)hipEventRecord(e1);
   if (hipEventSynchronize(e1) != hipSuccess) return 4;
   float ms = 0;
@@ -267,8 +302,8 @@ int main(int argc, char** argv) {
   const double us = ms * 1000.0 / iters;
   const double bytes = (double)nx * 2 + (double)ny2 * 2 + (double)ny3 * 2;
   const double flops = 2.0 * B * H * W * ((double)C * CM + (double)CM * CO) + 2.0 * ny3 * CM;
-  printf("chainbench B=%d %dx%d: %.1f us per launch (%.2f TB/s of boundary bytes, %.0f TF/s); max |d| y2 %.3g y3 %.3g, "
+  printf("chainbench %s B=%d %dx%d: %.1f us per launch (%.2f TB/s of boundary bytes, %.0f TF/s); max |d| y2 %.3g y3 %.3g, "
          "%d outside tolerance %s\n",
-         B, H, W, us, bytes / us / 1e6, flops / us / 1e6, md2, md3, bad, bad ? "FAIL" : "OK");
+         dma ? "dma" : "regs", B, H, W, us, bytes / us / 1e6, flops / us / 1e6, md2, md3, bad, bad ? "FAIL" : "OK");
   return bad ? 1 : 0;
 }
