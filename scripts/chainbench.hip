@@ -46,7 +46,9 @@ __device__ __forceinline__ uint32_t pool2x2(uint32_t r0, uint32_t r1) {
 }
 
 // x [B][H][W][256], W1 [256][256], W2p / W3p [128][256] (k permuted), y2 [B][H][W][128], y3 [B][H/2][W/2][128]
-template <bool DMA>
+// HOOK (attribution only, results then wrong): 1 x loaded for the first unit only, 2 no y2 / y3 MFMAs,
+// 4 no output stores, 8 no W1 ring traffic and no barriers
+template <bool DMA, int HOOK = 0>
 __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restrict__ x, const _Float16* __restrict__ W1,
                                                       const float* __restrict__ b1, const _Float16* __restrict__ W2p,
                                                       const float* __restrict__ b2, const _Float16* __restrict__ W3p,
@@ -102,17 +104,19 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
   const int nu = (U + waves - 1) / waves;       // every wave runs nu units (barriers are block-wide)
   const int gw = blockIdx.x * 8 + wave;
   int buf = 0;
+  u4 xs[2][8];
   for (int it = 0; it < nu; ++it) {
     const int u0 = gw + it * waves;
     const bool valid = u0 < U;
     const int u = valid ? u0 : 0;
     const int xs0 = (u % segs) * 16, y0 = ((u / segs) % rps) * 2, b = u / (segs * rps);
-    u4 xs[2][8];
+    if ((HOOK & 1) && it > 0) goto have_x;
 #pragma unroll
     for (int r = 0; r < 2; ++r)
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks)
         xs[r][ks] = *reinterpret_cast<const u4*>(x + ((size_t)(b * H + y0 + r) * W + xs0 + li) * C + ks * 32 + g * 8);
+  have_x:
     f4 acc2[8][2], acc3[8];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
@@ -125,7 +129,7 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
     // then its LDS write and the block barrier
     auto chunk = [&](int c, f4 (&a1)[2]) __attribute__((always_inline)) {
       u4 nxt;
-      if constexpr (DMA) w1dma((c + 2) & 15, (n + 2) % 3);   // two chunks ahead into the buffer read at n - 1
+      if constexpr (DMA && !(HOOK & 8)) w1dma((c + 2) & 15, (n + 2) % 3);   // two chunks ahead into the buffer read at n - 1
       else nxt = w1load((c + 1) & 15);      // the next chunk (the next unit's chunk 0 after c = 15)
       const unsigned char* w1b = smem + W1OFF + (DMA ? n % 3 : buf) * W1CH;
       const f4 bv1 = *reinterpret_cast<const f4*>(bl + c * 16 + g * 4);
@@ -138,7 +142,9 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
         for (int r = 0; r < 2; ++r)
           a1[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wf), __builtin_bit_cast(h8, xs[r][ks]), a1[r], 0, 0, 0);
       }
-      if constexpr (DMA) {
+      if constexpr (HOOK & 8) {
+        ++n;
+      } else if constexpr (DMA) {
         // chunk n + 1 (issued one step ago) has landed: younger VMEM ops are chunk n + 2's DMA only
         // (or, at a unit's first step, also this unit's X loads and the last unit's stores: waited too)
         asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
@@ -170,6 +176,10 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
       const u4 pm = {pool2x2(mid[0].x, mid[1].x), pool2x2(mid[0].y, mid[1].y), pool2x2(mid[0].z, mid[1].z),
                      pool2x2(mid[0].w, mid[1].w)};
       const int kq = s2 * 4 + g;                  // 16-byte chunk of the 32-channel k step s2
+      if constexpr (HOOK & 2) {
+        acc2[0][0][0] += __builtin_bit_cast(float, pm.x ^ mid[0].y ^ mid[1].z);
+        continue;
+      }
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         const u4 w2f = *reinterpret_cast<const u4*>(smem + W2OFF + slot(j * 16 + li, kq));
@@ -180,7 +190,7 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
         acc3[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w3f), __builtin_bit_cast(h8, pm), acc3[j], 0, 0, 0);
       }
     }
-    if (valid) {
+    if (valid && !(HOOK & 4)) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
 #pragma unroll
@@ -246,9 +256,17 @@ int main(int argc, char** argv) {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const int grid = cus;
   const bool dma = argc > 2 && argv[2][0] == 'd';
+  const int hook = argc > 3 ? atoi(argv[3]) : 0;
   auto launch = [&] {
-    if (dma) chain_kernel<true><<<grid, NTH>>>(dx, dW1, db1, dW2p, db2, dW3p, db3, dy2, dy3, B, H, W);
-    else chain_kernel<false><<<grid, NTH>>>(dx, dW1, db1, dW2p, db2, dW3p, db3, dy2, dy3, B, H, W);
+#define CB_L(D, HK) chain_kernel<D, HK><<<grid, NTH>>>(dx, dW1, db1, dW2p, db2, dW3p, db3, dy2, dy3, B, H, W)
+    if (!dma) CB_L(false, 0);
+    else if (hook == 1) CB_L(true, 1);
+    else if (hook == 2) CB_L(true, 2);
+    else if (hook == 4) CB_L(true, 4);
+    else if (hook == 8) CB_L(true, 8);
+    else if (hook == 15) CB_L(true, 15);
+    else CB_L(true, 0);
+#undef CB_L
   };
   (void)hipMemset(dy2, 0, ny2 * 2);
   (void)hipMemset(dy3, 0, ny3 * 2);
@@ -302,8 +320,9 @@ int main(int argc, char** argv) {
   const double us = ms * 1000.0 / iters;
   const double bytes = (double)nx * 2 + (double)ny2 * 2 + (double)ny3 * 2;
   const double flops = 2.0 * B * H * W * ((double)C * CM + (double)CM * CO) + 2.0 * ny3 * CM;
+  if (hook) printf("[hook %d] ", hook);
   printf("chainbench %s B=%d %dx%d: %.1f us per launch (%.2f TB/s of boundary bytes, %.0f TF/s); max |d| y2 %.3g y3 %.3g, "
          "%d outside tolerance %s\n",
          dma ? "dma" : "regs", B, H, W, us, bytes / us / 1e6, flops / us / 1e6, md2, md3, bad, bad ? "FAIL" : "OK");
-  return bad ? 1 : 0;
+  return (bad && !hook) ? 1 : 0;
 }
