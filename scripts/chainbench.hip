@@ -48,32 +48,36 @@ __device__ __forceinline__ uint32_t pool2x2(uint32_t r0, uint32_t r1) {
 // x [B][H][W][256], W1 [256][256], W2p / W3p [128][256] (k permuted), y2 [B][H][W][128], y3 [B][H/2][W/2][128]
 // HOOK (attribution only, results then wrong): 1 x loaded for the first unit only, 2 no y2 / y3 MFMAs,
 // 4 no output stores, 8 no W1 ring traffic and no barriers
-template <bool DMA, int HOOK = 0>
-__global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restrict__ x, const _Float16* __restrict__ W1,
+// RPW: image rows per wave-unit (2: 8 waves per block; 4: 4 waves, one per SIMD, every weight fragment
+// feeding twice the MFMAs)
+template <bool DMA, int HOOK = 0, int RPW = 2>
+__global__ __launch_bounds__(RPW == 2 ? 512 : 256, 1) void chain_kernel(const _Float16* __restrict__ x, const _Float16* __restrict__ W1,
                                                       const float* __restrict__ b1, const _Float16* __restrict__ W2p,
                                                       const float* __restrict__ b2, const _Float16* __restrict__ W3p,
                                                       const float* __restrict__ b3, _Float16* __restrict__ y2,
                                                       _Float16* __restrict__ y3, int B, int H, int W) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
   float* bl = reinterpret_cast<float*>(smem + BOFF);
+  constexpr int NT = RPW == 2 ? 512 : 256, NW = NT / 64, WI = 8192 / NT;
+  static_assert(DMA || RPW == 2, "the register-staged W1 ring is the 8-wave form only");
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, g = lane >> 4, li = lane & 15;
   // resident W2 / W3 (all loads first, then the LDS writes)
   {
-    u4 v[16];
+    u4 v[WI];
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int i = tid + t * NTH;           // 0 .. 8191: 2 x 128 rows x 32 chunks
+    for (int t = 0; t < WI; ++t) {
+      const int i = tid + t * NT;            // 0 .. 8191: 2 x 128 rows x 32 chunks
       const int m = i >> 12, r = (i >> 5) & 127, q = i & 31;
       const _Float16* src = (m ? W3p : W2p) + r * CM + q * 8;
       v[t] = *reinterpret_cast<const u4*>(src);
     }
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const int i = tid + t * NTH;
+    for (int t = 0; t < WI; ++t) {
+      const int i = tid + t * NT;
       const int m = i >> 12, r = (i >> 5) & 127, q = i & 31;
       *reinterpret_cast<u4*>(smem + (m ? W3OFF : W2OFF) + slot(r, q)) = v[t];
     }
-    bl[tid] = tid < CM ? b1[tid] : (tid < CM + CO ? b2[tid - CM] : b3[tid - CM - CO]);
+    for (int i = tid; i < CM + 2 * CO; i += NT) bl[i] = i < CM ? b1[i] : (i < CM + CO ? b2[i - CM] : b3[i - CM - CO]);
   }
   // W1 chunk c: thread tid moves row tid / 32, chunk tid % 32
   const int w1r = tid >> 5, w1q = tid & 31;
@@ -82,11 +86,16 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
   // DMA form: wave w's lane l moves row 2 w + l / 32, LDS slot l % 32 of a chunk, i.e. source chunk
   // (l % 32) ^ (row & 15) — the swizzle applied on the source side (the DMA writes 16 B per lane in lane order)
   const auto w1rs = __builtin_amdgcn_make_buffer_rsrc(const_cast<_Float16*>(W1), (short)0, CM * C * 2, 0x00020000);
-  const int dr = 2 * wave + (lane >> 5), dq = (lane & 31) ^ (dr & 15);
+  // (RPW 4: four waves, each moving pieces wave and wave + 4)
   auto w1dma = [&](int c, int b) __attribute__((always_inline)) {
-    __builtin_amdgcn_raw_ptr_buffer_load_lds(
-        w1rs, (__attribute__((address_space(3))) void*)(smem + W1OFF + b * W1CH + wave * 1024), 16,
-        (uint32_t)(((c * 16 + dr) * C + dq * 8) * 2), 0, 0, 0);
+#pragma unroll
+    for (int pc = 0; pc < 8 / NW; ++pc) {
+      const int piece = wave + pc * NW;
+      const int dr = 2 * piece + (lane >> 5), dq = (lane & 31) ^ (dr & 15);
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          w1rs, (__attribute__((address_space(3))) void*)(smem + W1OFF + b * W1CH + piece * 1024), 16,
+          (uint32_t)(((c * 16 + dr) * C + dq * 8) * 2), 0, 0, 0);
+    }
   };
   if constexpr (DMA) {
     w1dma(0, 0);
@@ -98,48 +107,50 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
   __syncthreads();
   int n = 0;   // W1 chunk sequence number (DMA ring position n % 3)
 
-  const int segs = W / 16, rps = H / 2;
+  const int segs = W / 16, rps = H / RPW;
   const int U = B * rps * segs;
-  const int waves = gridDim.x * 8;
+  const int waves = gridDim.x * NW;
   const int nu = (U + waves - 1) / waves;       // every wave runs nu units (barriers are block-wide)
-  const int gw = blockIdx.x * 8 + wave;
+  const int gw = blockIdx.x * NW + wave;
   int buf = 0;
-  u4 xs[2][8];
+  u4 xs[RPW][8];
   for (int it = 0; it < nu; ++it) {
     const int u0 = gw + it * waves;
     const bool valid = u0 < U;
     const int u = valid ? u0 : 0;
-    const int xs0 = (u % segs) * 16, y0 = ((u / segs) % rps) * 2, b = u / (segs * rps);
+    const int xs0 = (u % segs) * 16, y0 = ((u / segs) % rps) * RPW, b = u / (segs * rps);
     if ((HOOK & 1) && it > 0) goto have_x;
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+    for (int r = 0; r < RPW; ++r)
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks)
         xs[r][ks] = *reinterpret_cast<const u4*>(x + ((size_t)(b * H + y0 + r) * W + xs0 + li) * C + ks * 32 + g * 8);
   have_x:
-    f4 acc2[8][2], acc3[8];
+    f4 acc2[8][RPW], acc3[8][RPW / 2];
 #pragma unroll
     for (int j = 0; j < 8; ++j) {
       const f4 bv2 = *reinterpret_cast<const f4*>(bl + CM + j * 16 + g * 4);
-      acc2[j][0] = bv2;
-      acc2[j][1] = bv2;
-      acc3[j] = *reinterpret_cast<const f4*>(bl + CM + CO + j * 16 + g * 4);
+      const f4 bv3 = *reinterpret_cast<const f4*>(bl + CM + CO + j * 16 + g * 4);
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) acc2[j][r] = bv2;
+#pragma unroll
+      for (int r = 0; r < RPW / 2; ++r) acc3[j][r] = bv3;
     }
     // one W1 chunk: y1 rows 16 c .. +15 for both pixel rows; the next chunk's load in flight meanwhile,
     // then its LDS write and the block barrier
-    auto chunk = [&](int c, f4 (&a1)[2]) __attribute__((always_inline)) {
+    auto chunk = [&](int c, f4 (&a1)[RPW]) __attribute__((always_inline)) {
       u4 nxt;
       if constexpr (DMA && !(HOOK & 8)) w1dma((c + 2) & 15, (n + 2) % 3);   // two chunks ahead into the buffer read at n - 1
       else nxt = w1load((c + 1) & 15);      // the next chunk (the next unit's chunk 0 after c = 15)
       const unsigned char* w1b = smem + W1OFF + (DMA ? n % 3 : buf) * W1CH;
       const f4 bv1 = *reinterpret_cast<const f4*>(bl + c * 16 + g * 4);
-      a1[0] = bv1;
-      a1[1] = bv1;
+#pragma unroll
+      for (int r = 0; r < RPW; ++r) a1[r] = bv1;
 #pragma unroll
       for (int ks = 0; ks < 8; ++ks) {
         const u4 wf = *reinterpret_cast<const u4*>(w1b + slot(li, ks * 4 + g));
 #pragma unroll
-        for (int r = 0; r < 2; ++r)
+        for (int r = 0; r < RPW; ++r)
           a1[r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wf), __builtin_bit_cast(h8, xs[r][ks]), a1[r], 0, 0, 0);
       }
       if constexpr (HOOK & 8) {
@@ -147,7 +158,8 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
       } else if constexpr (DMA) {
         // chunk n + 1 (issued one step ago) has landed: younger VMEM ops are chunk n + 2's DMA only
         // (or, at a unit's first step, also this unit's X loads and the last unit's stores: waited too)
-        asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        if constexpr (NW == 8) asm volatile("s_waitcnt vmcnt(1)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
         __builtin_amdgcn_s_barrier();   // raw: __syncthreads' fence would drain chunk n + 2's DMA too
         ++n;
       } else {
@@ -158,13 +170,13 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
     };
 #pragma unroll 1
     for (int s2 = 0; s2 < 8; ++s2) {
-      f4 prev[2], a1[2];
+      f4 prev[RPW], a1[RPW];
       chunk(2 * s2, prev);
       chunk(2 * s2 + 1, a1);
       // mid channels 32 s2 + 4 g .. +3 (prev) and 32 s2 + 16 + 4 g .. +3 (a1): this lane's k values
-      u4 mid[2];
+      u4 mid[RPW];
 #pragma unroll
-      for (int r = 0; r < 2; ++r) {
+      for (int r = 0; r < RPW; ++r) {
         h8 m;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -173,11 +185,14 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
         }
         mid[r] = __builtin_bit_cast(u4, m);
       }
-      const u4 pm = {pool2x2(mid[0].x, mid[1].x), pool2x2(mid[0].y, mid[1].y), pool2x2(mid[0].z, mid[1].z),
-                     pool2x2(mid[0].w, mid[1].w)};
+      u4 pm[RPW / 2];
+#pragma unroll
+      for (int h = 0; h < RPW / 2; ++h)
+        pm[h] = u4{pool2x2(mid[2 * h].x, mid[2 * h + 1].x), pool2x2(mid[2 * h].y, mid[2 * h + 1].y),
+                   pool2x2(mid[2 * h].z, mid[2 * h + 1].z), pool2x2(mid[2 * h].w, mid[2 * h + 1].w)};
       const int kq = s2 * 4 + g;                  // 16-byte chunk of the 32-channel k step s2
       if constexpr (HOOK & 2) {
-        acc2[0][0][0] += __builtin_bit_cast(float, pm.x ^ mid[0].y ^ mid[1].z);
+        acc2[0][0][0] += __builtin_bit_cast(float, pm[0].x ^ mid[0].y ^ mid[1].z);
         continue;
       }
 #pragma unroll
@@ -185,16 +200,18 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
         const u4 w2f = *reinterpret_cast<const u4*>(smem + W2OFF + slot(j * 16 + li, kq));
         const u4 w3f = *reinterpret_cast<const u4*>(smem + W3OFF + slot(j * 16 + li, kq));
 #pragma unroll
-        for (int r = 0; r < 2; ++r)
+        for (int r = 0; r < RPW; ++r)
           acc2[j][r] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w2f), __builtin_bit_cast(h8, mid[r]), acc2[j][r], 0, 0, 0);
-        acc3[j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w3f), __builtin_bit_cast(h8, pm), acc3[j], 0, 0, 0);
+#pragma unroll
+        for (int h = 0; h < RPW / 2; ++h)
+          acc3[j][h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w3f), __builtin_bit_cast(h8, pm[h]), acc3[j][h], 0, 0, 0);
       }
     }
     if (valid && !(HOOK & 4)) {
 #pragma unroll
       for (int j = 0; j < 8; ++j)
 #pragma unroll
-        for (int r = 0; r < 2; ++r) {
+        for (int r = 0; r < RPW; ++r) {
           h4 o;
 #pragma unroll
           for (int i = 0; i < 4; ++i) o[i] = (_Float16)silu(acc2[j][r][i]);
@@ -202,13 +219,15 @@ __global__ __launch_bounds__(NTH, 1) void chain_kernel(const _Float16* __restric
         }
       if ((li & 1) == 0) {
 #pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          h4 o;
+        for (int j = 0; j < 8; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i) o[i] = (_Float16)silu(acc3[j][i]);
-          *reinterpret_cast<u2*>(y3 + ((size_t)(b * (H / 2) + y0 / 2) * (W / 2) + (xs0 + li) / 2) * CO + j * 16 + g * 4) =
-              __builtin_bit_cast(u2, o);
-        }
+          for (int h = 0; h < RPW / 2; ++h) {
+            h4 o;
+#pragma unroll
+            for (int i = 0; i < 4; ++i) o[i] = (_Float16)silu(acc3[j][h][i]);
+            *reinterpret_cast<u2*>(y3 + ((size_t)(b * (H / 2) + y0 / 2 + h) * (W / 2) + (xs0 + li) / 2) * CO + j * 16 + g * 4) =
+                __builtin_bit_cast(u2, o);
+          }
       }
     }
   }
@@ -256,10 +275,12 @@ int main(int argc, char** argv) {
   (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0);
   const int grid = cus;
   const bool dma = argc > 2 && argv[2][0] == 'd';
+  const bool rpw4 = argc > 2 && argv[2][0] == '4';   // "4": the four-row, one-wave-per-SIMD form (LDS-DMA ring)
   const int hook = argc > 3 ? atoi(argv[3]) : 0;
   auto launch = [&] {
 #define CB_L(D, HK) chain_kernel<D, HK><<<grid, NTH>>>(dx, dW1, db1, dW2p, db2, dW3p, db3, dy2, dy3, B, H, W)
-    if (!dma) CB_L(false, 0);
+    if (rpw4) chain_kernel<true, 0, 4><<<grid, 256>>>(dx, dW1, db1, dW2p, db2, dW3p, db3, dy2, dy3, B, H, W);
+    else if (!dma) CB_L(false, 0);
     else if (hook == 1) CB_L(true, 1);
     else if (hook == 2) CB_L(true, 2);
     else if (hook == 4) CB_L(true, 4);
@@ -323,6 +344,6 @@ int main(int argc, char** argv) {
   if (hook) printf("[hook %d] ", hook);
   printf("chainbench %s B=%d %dx%d: %.1f us per launch (%.2f TB/s of boundary bytes, %.0f TF/s); max |d| y2 %.3g y3 %.3g, "
          "%d outside tolerance %s\n",
-         dma ? "dma" : "regs", B, H, W, us, bytes / us / 1e6, flops / us / 1e6, md2, md3, bad, bad ? "FAIL" : "OK");
+         rpw4 ? "dma-4rows" : dma ? "dma" : "regs", B, H, W, us, bytes / us / 1e6, flops / us / 1e6, md2, md3, bad, bad ? "FAIL" : "OK");
   return (bad && !hook) ? 1 : 0;
 }
