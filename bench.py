@@ -164,14 +164,38 @@ def _cpu_quota():
         return None
 
 
+def map_parity(net, fused, img, plan, dev, frames=16, batch=32):
+    """mAP@0.5 (and @.5:.95) of the GPU plan's detections on `frames` synthetic frames (seed 7) against
+    the oracle's fp32 detections as ground truth (detect.py settings, conf 0.25 / iou 0.45), scored with
+    the product's test.py-style mAP (utils/metrics.py).  The frames run in one batch of `batch` (repeated
+    to fill it), so the plan takes the bench's own dispatch (bs 32) and the first `frames` are scored."""
+    from oracle import nms_ref, yolo_ref
+    from utils.general import nms_batched
+    from utils.metrics import dets_as_labels, map_from_lists
+    from yv7.synthetic import synthetic_frames
+    xs = synthetic_frames(frames, img, img, seed=7)
+    with torch.no_grad():
+        zr = torch.cat([yolo_ref.forward(net, fused, xs[i:i + 1])[0] for i in range(frames)])
+    labels = [dets_as_labels(d) for d in nms_ref.non_max_suppression(zr, 0.25, 0.45)]
+    xb = xs.repeat((batch + frames - 1) // frames, 1, 1, 1)[:max(batch, frames)]
+    N = plan.num_rows(img, img)
+    zg = torch.empty((xb.shape[0], N, plan.no), dtype=torch.float32, device=dev)
+    plan.forward_into(xb.to(dev).to(torch.float16 if plan.dtype == 1 else torch.float32), zg)
+    det, _, cnt = nms_batched(zg[:frames].contiguous(), 0.25, 0.45)
+    preds = [det[i, :int(cnt[i])].cpu() for i in range(frames)]
+    m50, m5095 = map_from_lists(preds, labels)
+    return {'map50': round(m50, 4), 'map50_95': round(m5095, 4), 'frames': frames, 'batch': int(xb.shape[0]),
+            'truth': 'oracle fp32 CPU detections (conf 0.25, iou 0.45)',
+            'pred': 'libyv7 plan (in a batch of %d: the bench dispatch) + GPU NMS, same frames and weights' % xb.shape[0]}
+
+
 def cpu_baseline(model_name, img, seconds, plan=None, dev=None, parity_frames=16, big_batch=32):
     """The oracle (reference CPU path restated) on the host cores this job may use: forward + NMS,
     timed separately like detect.py:142-153 (t2 - t1 forward, t3 - t2 NMS), at batch 1 (detect.py's
     loop; `value`) for about `seconds`, and one batch of `big_batch` frames (test.py's batch size).
 
-    Also the metric's parity half: on `parity_frames` synthetic frames the oracle's fp32 detections
-    (detect.py settings, conf 0.25 / iou 0.45) are the ground truth for the GPU fp16 plan's
-    detections, scored with the product's test.py-style mAP (utils/metrics.py)."""
+    Also the metric's parity half (map_parity): on `parity_frames` synthetic frames the oracle's fp32
+    detections are the ground truth for the GPU plan's."""
     from oracle import nms_ref, yolo_ref
     from models.yolo import Model
     from yv7.synthetic import synthetic_frames, synthetic_state_dict
@@ -212,21 +236,7 @@ def cpu_baseline(model_name, img, seconds, plan=None, dev=None, parity_frames=16
            f'batch{big_batch}': {'images_per_s': round(nb * big_batch / (fb + sb), 3),
                                  'forward_ms': round(fb / nb * 1e3, 1), 'nms_ms': round(sb / nb * 1e3, 2)}}
     if plan is not None and parity_frames > 0:
-        from utils.general import nms_batched
-        from utils.metrics import dets_as_labels, map_from_lists
-        xs = synthetic_frames(parity_frames, img, img, seed=7)
-        with torch.no_grad():
-            zr = torch.cat([yolo_ref.forward(net, fused, xs[i:i + 1])[0] for i in range(parity_frames)])
-        labels = [dets_as_labels(d) for d in nms_ref.non_max_suppression(zr, 0.25, 0.45)]
-        N = plan.num_rows(img, img)
-        zg = torch.empty((parity_frames, N, plan.no), dtype=torch.float32, device=dev)
-        plan.forward_into(xs.to(dev).to(torch.float16 if plan.dtype == 1 else torch.float32), zg)
-        det, _, cnt = nms_batched(zg, 0.25, 0.45)
-        preds = [det[i, :int(cnt[i])].cpu() for i in range(parity_frames)]
-        m50, m5095 = map_from_lists(preds, labels)
-        out['map_parity'] = {'map50': round(m50, 4), 'map50_95': round(m5095, 4), 'frames': parity_frames,
-                             'truth': 'oracle fp32 CPU detections (conf 0.25, iou 0.45)',
-                             'pred': 'libyv7 plan + GPU NMS, same frames and weights'}
+        out['map_parity'] = map_parity(net, fused, img, plan, dev, parity_frames)
     return out
 
 
@@ -422,7 +432,7 @@ def main(argv=None):
     from yv7 import _lib as L
     from yv7.runtime import kernel_key
     costs = plan.op_costs(B, H, W, x_bytes=x.element_size(), with_raw=False)
-    kernels = plan.op_kernels(B, H, W)
+    kernels = plan.op_kernels(B, H, W, x.dtype)
 
     def conv_family(nf, op_ms):
         """(mean conv/DETECT launch s, bytes per launch, flops per launch, launches, forward ms, conv ms)."""
@@ -442,8 +452,17 @@ def main(argv=None):
         mean launch us, algorithmic bytes / FLOPs per launch, roof us = max(bytes / 8 TB/s, FLOPs / 2.5
         PF), frac = roof / time, the binding roof."""
         fam = {}
+        f = None
         for i, ((kind, fl, by), ms) in enumerate(zip(costs, op_ms)):
             if not kernels[i]:
+                # an op without a kernel of its own (the second op of the dual 1x1 launch, the later pools
+                # of the SPPCSPC cascade) ran inside the launch before it: its bytes and FLOPs (and its
+                # zero-length event interval) belong to that kernel (ADVICE r3)
+                if f is not None:
+                    f['ms'] += ms / max(nf, 1)
+                    f['bytes'] += by
+                    f['flops'] += fl
+                    f['ops'].append(i)
                 continue
             k = kernel_key(kernels[i][-1])
             f = fam.setdefault(k, {'kernel': k, 'launches': 0, 'ms': 0.0, 'bytes': 0.0, 'flops': 0.0, 'ops': []})

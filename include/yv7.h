@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-#define YV7_ABI_VERSION 3
+#define YV7_ABI_VERSION 4
 
 /* Activation tensors in the forward workspace are NHWC with a YV7_BORDER-pixel zero frame around
  * every image: [B][h + 2*YV7_BORDER][w + 2*YV7_BORDER][C].  Kernels write only interiors; the frame
@@ -146,8 +146,10 @@ int yv7_forward(yv7_plan* plan, const void* x, int x_dtype, int B, int H, int W,
 /* The kernels the dispatch launches for every op of a [B,3,H,W] forward, without running it (a dry
  * run of yv7_forward's op loop): one line per op, "op<TAB>kernel[|kernel...]", kernel = the demangled
  * symbol rocprofv3's kernel trace reports.  Lets a caller attribute per-op timings (yv7_profile_read)
- * to kernel families.  Needs the plan's device to be current; buf receives a NUL-terminated string. */
-int yv7_op_kernels(yv7_plan* plan, int B, int H, int W, char* buf, size_t bytes);
+ * to kernel families.  x_dtype: the image dtype the forward would get (the INPUT / STEM kernels depend on
+ * it).  An op that would launch more than 4 kernels is an error.  Needs the plan's device to be current;
+ * buf receives a NUL-terminated string. */
+int yv7_op_kernels(yv7_plan* plan, int B, int H, int W, int x_dtype, char* buf, size_t bytes);
 
 /* Force the kernel configuration of one CONV / DETECT op (0 = the tuned dispatch, the default).  For
  * parity tests of every kernel variant and A/B timing; the accepted values are the real kernel

@@ -23,6 +23,16 @@ __global__ void fill_rand(_Float16* p, size_t n, uint32_t seed, float scale) {
   }
 }
 
+// the conv kernels read a 3x3 window's out-of-image taps from the tensor's zero frame (yv7_kernels.h)
+__global__ void zero_frame(_Float16* x, int B, int H, int W, int C) {
+  const size_t n = yv7::bordered_pixels(B, H, W);
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) {
+    const int w = (int)(i % (W + 2)), h = (int)((i / (W + 2)) % (H + 2));
+    if (h == 0 || h == H + 1 || w == 0 || w == W + 1)
+      for (int c = 0; c < C; ++c) x[i * C + c] = (_Float16)0.0f;
+  }
+}
+
 int main(int argc, char** argv) {
   std::vector<Shape> shapes = {
     {"3x3 64->64 @320", 32, 320, 320, 64, 64, 3, 1},
@@ -82,6 +92,8 @@ int main(int argc, char** argv) {
   void* zero;
   CK(hipMalloc(&x, maxx * 2)); CK(hipMalloc(&y, maxy * 2)); CK(hipMalloc(&y0, maxy * 2)); CK(hipMalloc(&w, maxw * 2));
   CK(hipMalloc(&b, 8192 * 4)); CK(hipMalloc(&zero, 4096)); CK(hipMemset(zero, 0, 4096));
+  void* wf;   // fragment-packed 3x3 weights (conv_lr.hip, variants 270-274)
+  CK(hipMalloc(&wf, maxw * 2));
   const size_t part_bytes = (size_t)512 << 20;
   const int cnt_n = 1 << 20;
   float* part; int* cnt;
@@ -96,6 +108,8 @@ int main(int argc, char** argv) {
     if (filt && !strstr(s.name, filt)) continue;
     yv7::ConvParams p; memset(&p, 0, sizeof(p));
     p.x = x; p.y = y; p.w = w; p.bias = b; p.zero = zero;
+    hipLaunchKernelGGL(fill_rand, dim3(4096), dim3(256), 0, 0, x, maxx, 1u, 1.0f);
+    hipLaunchKernelGGL(zero_frame, dim3(1024), dim3(256), 0, 0, x, s.B, s.H, s.W, s.cin);
     p.part = part; p.cnt = cnt; p.part_bytes = part_bytes; p.cnt_n = cnt_n;
     p.B = s.B; p.H = s.H; p.W = s.W; p.xc = s.cin; p.xoff = 0; p.cin = s.cin;
     p.k = s.k; p.s = s.s; p.pad = s.k / 2;
@@ -109,6 +123,11 @@ int main(int argc, char** argv) {
     for (int n = 0; n < s.cout; ++n)
       hipLaunchKernelGGL(fill_rand, dim3(4), dim3(256), 0, 0, w + (size_t)n * p.kpad, (size_t)p.K, 7u + n,
                          1.0f / sqrtf((float)p.K));
+    if (s.k == 3 && s.s == 1 && s.cin % 32 == 0) {
+      CK(yv7::pack_frag3x3(w, p.kpad, s.cin, s.cout, wf, 0));
+      p.wf = wf;
+      p.wfbytes = (uint32_t)yv7::frag3x3_bytes(s.cin, s.cout);
+    }
     const size_t ny = yv7::bordered_pixels(s.B, p.Ho, p.Wo) * s.cout;
     double flops = 2.0 * p.M * s.cout * p.K;
     double bytes = 2.0 * ((double)s.B * s.H * s.W * s.cin + (double)ny);

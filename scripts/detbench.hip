@@ -30,7 +30,8 @@ int main(int argc, char** argv) {
   }
   CK(hipMemset(b, 0, 256 * 4)); CK(hipMemset(zero, 0, 4096));
   std::vector<int> variants = {0, 92, 97};
-  if (argc > 1) {   // e.g. 0,90,91,93,94 (hooks: 90 GEMM only, 91 epilogue only, 93 no z / row-score stores, 94 no K loop)
+  if (argc > 1) {   // e.g. 0,92,97,98,99 (98: the persistent head without its sigmoid staging; the round-2
+                    // tile-kernel hooks 90-96 were removed in round 4, see DESIGN §4.2 for their results)
     variants.clear();
     for (char* t = strtok(argv[1], ","); t; t = strtok(nullptr, ",")) variants.push_back(atoi(t));
   }

@@ -35,7 +35,8 @@ for step in "$@"; do
   echo "== $step"
   case "$name" in
     tests)
-      timeout -k 10 600 python -u -m pytest ${arg:-tests} -m gpu -x -v --timeout 300 --timeout-method thread -rf \
+      [ -z "$arg" ] && arg=tests
+      timeout -k 10 600 python -u -m pytest ${arg//,/ } -m gpu -x -v --timeout 300 --timeout-method thread -rf \
         > $O/tests.log 2>&1
       rc=$?; grep -E "passed|failed" $O/tests.log | tail -1; grep -E "^FAILED" $O/tests.log | head
       [ $rc -eq 0 ] || exit $rc ;;
@@ -50,7 +51,7 @@ for step in "$@"; do
     tune)
       IFS=: read -r ops cands rounds <<< "$arg"
       sel="--ops $ops"; [ "$ops" = all ] && sel=
-      timeout -k 10 1100 python -u scripts/tune_ops.py $sel --cands $cands --rounds ${rounds:-2} \
+      timeout -k 10 1100 python -u scripts/tune_ops.py $sel --cands $cands --rounds ${rounds:-2} $TUNE_ARGS \
         > $O/tune.txt 2>&1 || { tail -20 $O/tune.txt; exit 1; }
       grep -v amdgpu.ids $O/tune.txt | tail -90 ;;
     bench)

@@ -10,6 +10,7 @@ from yv7 import _lib as L
 ap = argparse.ArgumentParser(); ap.add_argument('--model', default='yolov7'); ap.add_argument('--b', type=int, default=32)
 ap.add_argument('--img', type=int, default=640); ap.add_argument('--dtype', default='f16'); ap.add_argument('--iters', type=int, default=10)
 ap.add_argument('--csv', default=''); ap.add_argument('--top', type=int, default=40)
+ap.add_argument('--dump', default='', help='JSON of every op: desc, kernels, us, algorithmic bytes (scripts/pmc_ops.py)')
 a = ap.parse_args()
 dt = torch.float32 if a.dtype == 'f32' else torch.float16
 m = Model(a.model); synthetic_state_dict(m, seed=0); m = m.float().fuse().eval()
@@ -37,6 +38,11 @@ for i, ((kind, fl, by), t, o) in enumerate(zip(costs, ms, plan.graph.ops)):
     # roofline-limited time at 8 TB/s and 2.5 PF
     tmin = max(by / 8e12, fl / 2.5e15) * 1e3
     rows.append((t, i, desc, tf, gb, tmin))
+if a.dump:
+    import json
+    ks = plan.op_kernels(B, H, H)
+    json.dump([{'op': i, 'desc': desc, 'us': t * 1e3, 'roof_us': tmin * 1e3, 'bytes': costs[i][2], 'flops': costs[i][1],
+                'kernels': ks[i]} for t, i, desc, tf, gb, tmin in sorted(rows, key=lambda r: r[1])], open(a.dump, 'w'), indent=0)
 print(f'forward {tot:.3f} ms over {n} forwards; sum of roofline minima {sum(r[5] for r in rows):.3f} ms')
 import csv
 if a.csv:

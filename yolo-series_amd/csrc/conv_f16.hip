@@ -267,14 +267,9 @@ __device__ __forceinline__ void det_epilogue(const ConvParams& p, unsigned char*
   det_table<BM, BN, NTH>(p, smem, m0, tid);
   __syncthreads();
   const bool std85 = p.no == 85 && p.na == 3;
-  if (p.variant == 95) {}   // microbenchmark hook (with 94's empty K loop): no sigmoid / decode staging
-  else if (std85) det_stage<BM, BN, TN, TM, 85, 3>(p, smem, acc, m0, wm, wn, g, li);
+  if (std85) det_stage<BM, BN, TN, TM, 85, 3>(p, smem, acc, m0, wm, wn, g, li);
   else det_stage<BM, BN, TN, TM, 0, 0>(p, smem, acc, m0, wm, wn, g, li);
   __syncthreads();
-  if (p.variant == 93) {   // microbenchmark hook: no z / row-score stores
-    if (reinterpret_cast<float*>(smem)[tid] == 12345.0f) p.z[tid] = 1.0f;
-    return;
-  }
   if (std85) det_tail<BM, BN, NTH, 85, 3>(p, smem, tid);
   else det_tail<BM, BN, NTH, 0, 0>(p, smem, tid);
 }
@@ -359,10 +354,7 @@ __device__ __forceinline__ void det_tail(const ConvParams& p, unsigned char* sme
       const long long z0 = t.zrow0[grp * 4];
       const f4 v = reinterpret_cast<const f4*>(zs + (a * BM + grp * 4) * NO)[c];
       if (z0 >= 0 && t.zrow0[grp * 4 + 3] == z0 + 3 && ((z0 + aoff) & 3) == 0) {
-        if (p.variant == 96)   // microbenchmark hook (with 94's empty K loop): temporal z stores
-          reinterpret_cast<f4*>(p.z + (size_t)(z0 + aoff) * NO)[c] = v;
-        else
-          __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p.z + (size_t)(z0 + aoff) * NO) + c);
+        __builtin_nontemporal_store(v, reinterpret_cast<f4*>(p.z + (size_t)(z0 + aoff) * NO) + c);
       } else {
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
@@ -763,8 +755,7 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
   u4 ra[RA], rb[RB];
   gload(0, ra, rb);
   lstore(0, ra, rb);
-  if (DET && p.variant == 91) {   // microbenchmark hook: epilogue only
-  } else if constexpr (PF == 1) {
+  if constexpr (PF == 1) {
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       if (kt + 1 < nk) gload(kt + 1, ra, rb);
@@ -793,10 +784,6 @@ __global__ __launch_bounds__(NT, 2) void conv_f16_kernel(const ConvParams p) {
 
   // accumulator acc[j][i][e]: output channel n = n0 + wn*WTN + j*16 + g*4 + e, pixel m = m0 + wm*WTM + i*16 + li
   if constexpr (DET) {
-    if (p.variant == 90) {   // microbenchmark hook: GEMM only
-      if (acc[0][0][0] == 12345.0f) p.z[tid] = acc[TN - 1][TM - 1][3];
-      return;
-    }
     det_epilogue<BM, BN, NT>(p, smem, acc, m0, wm, wn, g, li, tid);
     return;
   }
@@ -994,7 +981,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
     if (s0 < nk) issue(s0, s0);
 
   int slot = 0;
-  for (int kt = 0; kt < (DET && p.variant >= 94 && p.variant <= 96 ? 0 : nk); ++kt) {
+  for (int kt = 0; kt < nk; ++kt) {
     // stage kt must have landed; the (at most STAGES-2) stages issued after it may stay in flight
     const int ahead = nk - 1 - kt;
     if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
@@ -1039,10 +1026,6 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   if (S > 1 && !splitk_reduce<NTH, TN, TM>(p, smem, acc, tile, ks, S, tid)) return;
 
   if constexpr (DET) {
-    if (p.variant == 90) {   // microbenchmark hook: GEMM only
-      if (acc[0][0][0] == 12345.0f) p.z[tid] = acc[TN - 1][TM - 1][3];
-      return;
-    }
     det_epilogue<BM, BN, NTH>(p, smem, acc, m0, wm, wn, g, li, tid);
     return;
   }
@@ -2468,9 +2451,29 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // the register-streamed 1x1 (conv_rs.hip; 240 forces it where it applies)
   if (!det && variant == 240 && conv1x1_rs_supported(p, nullptr)) return launch_conv1x1_rs(p, nullptr, st);
   // the 3x3 halo ring (conv_hring.hip): 260 = 128-channel tiles, 261 = 256-channel tiles
+  // (forced only where every N tile is full: the masked last tile of a cout that 128 does not divide has
+  // no layer in the checked networks — ADVICE r3)
   if (!det && (variant == 260 || variant == 261 || variant == 262 || (variant >= 911 && variant <= 914)) &&
-      hring_supported(p))
+      hring_supported(p) && p.cout % (variant == 261 ? 256 : 128) == 0)
     return launch_conv_hring(p, variant == 261 ? 256 : variant == 260 ? 128 : 2, device_cus(), st);
+  // the low-resolution 3x3 kernel (conv_lr.hip): 270 + tile configuration
+  if (!det && variant >= 270 && variant <= 273 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
+  // 3x3 stride-1 layers up to 80 x 80 (every 3x3 s1 layer of yolov7 640 from 80^2 down, yolov7-w6 1280's
+  // from 80^2 down): the low-resolution kernel (conv_lr.hip) — one layer forced at a time in the bs-32
+  // forward (profiles/r4lr/tune3.txt, us, dispatch -> lr): 3x3 256->256 @20 32.2 -> 22.1, 512->512 @20
+  // 80.8 -> 62.7, 512->256 @20 48.8 -> 37.0, 512->1024 @20 119.8 -> 107.5, 128->128 @40 24.5 -> 21.9,
+  // 256->128 @40 43.5 -> 35.6, 256->256 @40 69.9 -> 59.5, 256->512 @40 129.8 -> 108.5, 128->128 @80
+  // 74.3 -> 63.4, 128->256 @80 123.9 -> 119.5, 128->64 @80 50.2 -> 40.8, 64->64 @80 31.6 -> 27.4.
+  // 80 x 128 tiles when there are >= 1000 of them, else 80 x 64 (64-pixel tiles when 5 does not divide
+  // the height).  YV7_LR=0: off.
+  static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
+  if (!det && variant == 0 && lr && p.H <= 80 && p.k == 3 && p.s == 1 &&
+      !((long)p.B * (p.H / 16) * (p.W / 16) >= 2048 && ws64_supported(p))) {
+    const bool t5 = p.H % 5 == 0;
+    const long t128 = (long)((p.B + 3) / 4) * (p.H / (t5 ? 5 : 4)) * (p.W / 4) * (p.cout / 128);
+    const int cfg = (p.cout % 128 == 0 && t128 >= 1000 ? 0 : 1) + (t5 ? 0 : 2);
+    if (lr_supported(p, cfg)) return launch_conv_lr(p, cfg, st);
+  }
   // 3x3 stride-1 layers with 128-channel output tiles and at least one round of 16 x 16 x 128 tiles: the
   // column-group halo ring (conv_hring.hip, variant 262).  Single-layer sweep, bs 32 640, same box
   // (profiles/r3_hring2_tune.txt, us, dispatch -> 262): 3x3 128->128 @80 80.0 / 80.4 / 82.7 / 81.0 ->

@@ -41,6 +41,10 @@ struct yv7_plan {
   void* weights = nullptr;
   size_t wbytes = 0;
   void* zero = nullptr;  // 4 KiB of zeros
+  // fp16 plans: every 3x3 stride-1 conv's weights again, fragment-packed for conv_lr.hip (pack_frag3x3);
+  // wf_off[op] = byte offset into wfrag, -1 when the op has none
+  void* wfrag = nullptr;
+  std::vector<int64_t> wf_off;
   // the workspaces whose zero frames are known to be intact for one layout (see yv7_forward); several,
   // so that batches in flight can run concurrently on their own streams and workspaces
   struct WsKey {
@@ -109,6 +113,11 @@ int kpad_of(const yv7_op_desc& o) {
   return (o.k * o.k * o.cin + 63) / 64 * 64;
 }
 bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7_WFMT_FP8; }
+// 3x3 / stride-1 / pad-1 fp16 convs get a fragment-packed weight copy (conv_lr.hip)
+bool wants_frag(int dtype, const yv7_op_desc& o) {
+  return dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && o.k == 3 && o.s == 1 && o.pad == 1 && !o.pool &&
+         o.cin % 32 == 0;
+}
 
 // Geometry / operand fields of a CONV or DETECT op's kernel parameters (pointers into the workspace
 // are filled by the caller).
@@ -138,6 +147,10 @@ yv7::ConvParams conv_params(const yv7_plan* p, size_t op, int B, int H, int W) {
   c.xbytes = (uint32_t)tensor_bytes(p, ti, B, H, W);
   c.wbytes = (uint32_t)((size_t)((o.cout + 31) / 32 * 32) * c.kpad * es);
   c.variant = p->op_variant[op];
+  if (p->wfrag && p->wf_off[op] >= 0) {
+    c.wf = reinterpret_cast<const unsigned char*>(p->wfrag) + p->wf_off[op];
+    c.wfbytes = (uint32_t)yv7::frag3x3_bytes(o.cin, o.cout);
+  }
   return c;
 }
 
@@ -278,6 +291,28 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
     delete p;
     return hip_fail(e, "hipMalloc(zero page)");
   }
+  // fragment-packed copies of the 3x3 stride-1 weights (conv_lr.hip), packed on the device from the
+  // plan's own copy
+  p->wf_off.assign(p->ops.size(), -1);
+  size_t wf_total = 0;
+  for (size_t i = 0; i < p->ops.size(); ++i)
+    if (wants_frag(p->dtype, p->ops[i])) {
+      p->wf_off[i] = (int64_t)wf_total;
+      wf_total = align256(wf_total + yv7::frag3x3_bytes(p->ops[i].cin, p->ops[i].cout));
+    }
+  if (wf_total) {
+    e = hipMalloc(&p->wfrag, wf_total);
+    for (size_t i = 0; e == hipSuccess && i < p->ops.size(); ++i)
+      if (p->wf_off[i] >= 0)
+        e = yv7::pack_frag3x3(reinterpret_cast<const unsigned char*>(p->weights) + p->ops[i].w_off, kpad_of(p->ops[i]),
+                              p->ops[i].cin, p->ops[i].cout, reinterpret_cast<unsigned char*>(p->wfrag) + p->wf_off[i],
+                              nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) {
+      yv7_plan_destroy(p);
+      return hip_fail(e, "yv7_plan_create: fragment packing");
+    }
+  }
   *out = p;
   return 0;
 }
@@ -329,6 +364,7 @@ void yv7_plan_destroy(yv7_plan* p) {
   free_events(p);
   if (p->weights) (void)hipFree(p->weights);
   if (p->zero) (void)hipFree(p->zero);
+  if (p->wfrag) (void)hipFree(p->wfrag);
   delete p;
 }
 
@@ -363,7 +399,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
   return (v >= 201 && v <= 206) || (v >= 211 && v <= 218) || (v >= 221 && v <= 223) || (v >= 231 && v <= 240) ||
-         (v >= 260 && v <= 262);
+         (v >= 260 && v <= 262) || (v >= 270 && v <= 273);
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {
@@ -562,9 +598,15 @@ static int forward_impl(yv7_plan* p, const void* x, int x_dtype, int B, int H, i
           if (dual && p->dtype == YV7_DT_F16 && i + 1 < p->ops.size() && p->op_variant[i] == 0 &&
               p->op_variant[i + 1] == 0) {
             const auto& o1 = p->ops[i + 1];
+            // one launch reads the shared slice while it writes both outputs: neither output may overlap
+            // the input slice or the other output (in order, op i + 1 would see op i's writes) — the
+            // hazards graph.py's _merge_siblings checks before its fusions
+            auto overlap = [](int ta, int ca, int na, int tb, int cb, int nb) { return ta == tb && ca < cb + nb && cb < ca + na; };
             const bool pair = o1.kind == YV7_OP_CONV && !is_f8(o1) && o1.src == o.src && o1.src_coff == o.src_coff &&
                               o1.cin == o.cin && o1.k == 1 && o.k == 1 && ((o.pool == 2) != (o1.pool == 2)) &&
-                              o1.w_off != o.w_off;
+                              o1.w_off != o.w_off && !overlap(o.dst, o.dst_coff, o.cout, o.src, o.src_coff, o.cin) &&
+                              !overlap(o1.dst, o1.dst_coff, o1.cout, o.src, o.src_coff, o.cin) &&
+                              !overlap(o.dst, o.dst_coff, o.cout, o1.dst, o1.dst_coff, o1.cout);
             if (pair) {
               const size_t fi = o.pool == 2 ? i + 1 : i, pi = o.pool == 2 ? i : i + 1;
               const auto& of = p->ops[fi];
@@ -686,7 +728,8 @@ static int forward_impl(yv7_plan* p, const void* x, int x_dtype, int B, int H, i
     if (e != hipSuccess) return hip_fail(e, "yv7_forward launch");
     if (dry) {
       const auto& r = yv7::launch_rec();
-      for (int k = 0; k < r.n && k < 4; ++k) (*kernels)[i].push_back(r.fn[k]);
+      if (r.n > 4) return fail(YV7_E_ARG, "yv7_op_kernels: op " + std::to_string(i) + " launches more than 4 kernels");
+      for (int k = 0; k < r.n; ++k) (*kernels)[i].push_back(r.fn[k]);
     }
     if (ev && yv7::op_events().launches == 0) {   // no kernel of its own (a later op of a fused cascade)
       if ((e = hipEventRecord(ev[2 * i], st)) != hipSuccess || (e = hipEventRecord(ev[2 * i + 1], st)) != hipSuccess)
@@ -707,13 +750,13 @@ int yv7_forward(yv7_plan* p, const void* x, int x_dtype, int B, int H, int W, fl
   return forward_impl(p, x, x_dtype, B, H, W, z, raw, rowbest, ws, ws_bytes, stream, nullptr);
 }
 
-int yv7_op_kernels(yv7_plan* p, int B, int H, int W, char* buf, size_t bytes) {
+int yv7_op_kernels(yv7_plan* p, int B, int H, int W, int x_dtype, char* buf, size_t bytes) {
   if (!p || !buf || bytes == 0) return fail(YV7_E_ARG, "yv7_op_kernels: null argument");
   std::vector<std::vector<const void*>> ks;
   // dry run: the op loop with placeholder pointers (nothing is launched or dereferenced on the host)
   static const float dummy[4] = {0, 0, 0, 0};
   void* ph = const_cast<float*>(dummy);
-  if (int rc = forward_impl(p, ph, YV7_DT_F16, B, H, W, static_cast<float*>(ph), nullptr, nullptr, ph, 0, nullptr, &ks))
+  if (int rc = forward_impl(p, ph, x_dtype, B, H, W, static_cast<float*>(ph), nullptr, nullptr, ph, 0, nullptr, &ks))
     return rc;
   std::string out;
   for (size_t i = 0; i < ks.size(); ++i) {

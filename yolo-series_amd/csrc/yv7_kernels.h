@@ -142,6 +142,10 @@ struct ConvParams {
   int cnt_n;
   int ksplit;
   int pool;           // 2: 1x1 conv over the 2x2 / stride-2 max of the input (MP folded in; k = 1, s = 2)
+  // 3x3 stride-1 convs of fp16 plans: the weights again, fragment-packed for conv_lr.hip (pack_frag3x3),
+  // or null
+  const void* wf;
+  uint32_t wfbytes;
 };
 
 // The max-pooled second consumer of a register-streamed 1x1 conv's input (conv_rs.hip): the MP block's
@@ -203,6 +207,11 @@ bool ws64_supported(const ConvParams& p);
 hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st);
 hipError_t launch_conv_halo(const ConvParams& p, hipStream_t st);
 bool hring_supported(const ConvParams& p);
+// low-resolution 3x3 (conv_lr.hip): cfg 0-4 = tile shape; weights from ConvParams::wf
+bool lr_supported(const ConvParams& p, int cfg);
+hipError_t launch_conv_lr(const ConvParams& p, int cfg, hipStream_t st);
+size_t frag3x3_bytes(int cin, int cout);
+hipError_t pack_frag3x3(const void* w, int kpad, int cin, int cout, void* out, hipStream_t st);
 hipError_t launch_conv_hring(const ConvParams& p, int bn, int cus, hipStream_t st);
 hipError_t launch_input(int dtype, const void* x, int x_dtype, void* y, int B, int H, int W, int yc,
                         bool reorg, hipStream_t st);

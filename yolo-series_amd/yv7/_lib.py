@@ -13,7 +13,7 @@ import os
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, 'libyv7.so')
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 BORDER = 1          # zero frame around every workspace tensor (YV7_BORDER)
 DT_F32, DT_F16 = 0, 1
 ACT_NONE, ACT_SILU, ACT_LEAKY = 0, 1, 2
@@ -60,7 +60,7 @@ SIGNATURES = {
     'yv7_set_op_variant': (_i, [_vp, _i, _i]),
     'yv7_num_rows': (_i64, [_vp, _i, _i]),
     'yv7_forward': (_i, [_vp, _vp, _i, _i, _i, _i, _vp, _vp, _vp, _vp, _sz, _vp]),
-    'yv7_op_kernels': (_i, [_vp, _i, _i, _i, ctypes.c_char_p, _sz]),
+    'yv7_op_kernels': (_i, [_vp, _i, _i, _i, _i, ctypes.c_char_p, _sz]),
     'yv7_profile_enable': (_i, [_vp, _i]),
     'yv7_profile_read': (_i, [_vp, ctypes.POINTER(_i), ctypes.POINTER(ctypes.c_float)]),
     'yv7_tensor_info': (_i, [_vp, _i, _i, _i, _i, ctypes.POINTER(_i64), ctypes.POINTER(_i64)]),

@@ -235,13 +235,14 @@ class Plan:
         L.check(L.lib().yv7_profile_read(self._h, ctypes.byref(n), ms), 'yv7_profile_read')
         return n.value, list(ms)
 
-    def op_kernels(self, B, H, W):
+    def op_kernels(self, B, H, W, x_dtype=None):
         """Per op, the kernel names (rocprofv3's demangled symbols) the dispatch launches for a
         [B,3,H,W] forward (yv7_op_kernels: a dry run, nothing executes); [] for an op without a
         kernel of its own (the later pools of the SPPCSPC cascade)."""
         buf = ctypes.create_string_buffer(1 << 20)
         with torch.cuda.device(self.device):
-            L.check(L.lib().yv7_op_kernels(self._h, B, H, W, buf, len(buf)), 'yv7_op_kernels')
+            xdt = L.DT_F16 if x_dtype in (None, torch.float16) else L.DT_F32
+            L.check(L.lib().yv7_op_kernels(self._h, B, H, W, xdt, buf, len(buf)), 'yv7_op_kernels')
         out = [[] for _ in self.graph.ops]
         for line in buf.value.decode().splitlines():
             i, _, names = line.partition('\t')
