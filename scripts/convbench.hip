@@ -123,7 +123,7 @@ int main(int argc, char** argv) {
     for (int n = 0; n < s.cout; ++n)
       hipLaunchKernelGGL(fill_rand, dim3(4), dim3(256), 0, 0, w + (size_t)n * p.kpad, (size_t)p.K, 7u + n,
                          1.0f / sqrtf((float)p.K));
-    if (s.k == 3 && s.s == 1 && s.cin % 32 == 0) {
+    if (s.k == 3 && s.cin % 32 == 0) {
       CK(yv7::pack_frag3x3(w, p.kpad, s.cin, s.cout, wf, 0));
       p.wf = wf;
       p.wfbytes = (uint32_t)yv7::frag3x3_bytes(s.cin, s.cout);

@@ -2458,8 +2458,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     return launch_conv_hring(p, variant == 261 ? 256 : variant == 260 ? 128 : 2, device_cus(), st);
   // the low-resolution 3x3 kernel (conv_lr.hip): 270 + tile configuration
   if (!det && variant >= 270 && variant <= 273 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
-  // 3x3 stride-1 layers up to 80 x 80 (every 3x3 s1 layer of yolov7 640 from 80^2 down, yolov7-w6 1280's
-  // from 80^2 down): the low-resolution kernel (conv_lr.hip) — one layer forced at a time in the bs-32
+  // 3x3 stride-1 layers of up to 204 800 output pixels (yolov7 640 bs 32 from 80^2 down, yolov7-w6 1280
+  // bs 8 from 160^2 down): the low-resolution kernel (conv_lr.hip) — one layer forced at a time in the bs-32
   // forward (profiles/r4lr/tune3.txt, us, dispatch -> lr): 3x3 256->256 @20 32.2 -> 22.1, 512->512 @20
   // 80.8 -> 62.7, 512->256 @20 48.8 -> 37.0, 512->1024 @20 119.8 -> 107.5, 128->128 @40 24.5 -> 21.9,
   // 256->128 @40 43.5 -> 35.6, 256->256 @40 69.9 -> 59.5, 256->512 @40 129.8 -> 108.5, 128->128 @80
@@ -2467,7 +2467,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // 80 x 128 tiles when there are >= 1000 of them, else 80 x 64 (64-pixel tiles when 5 does not divide
   // the height).  YV7_LR=0: off.
   static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
-  if (!det && variant == 0 && lr && p.H <= 80 && p.k == 3 && p.s == 1 &&
+  if (!det && variant == 0 && lr && (long)p.M <= 204800 && p.k == 3 && p.s == 1 &&
       !((long)p.B * (p.H / 16) * (p.W / 16) >= 2048 && ws64_supported(p))) {
     const bool t5 = p.H % 5 == 0;
     const long t128 = (long)((p.B + 3) / 4) * (p.H / (t5 ? 5 : 4)) * (p.W / 4) * (p.cout / 128);

@@ -34,19 +34,27 @@ namespace yv7 {
 namespace {
 
 constexpr int FI = 4, FC = 4;   // MFMA pixel fragment: 4 images x 4 columns
-constexpr int PC = FC + 2;      // patch columns
 constexpr int CK = 32;          // channels per chunk (one MFMA K step)
 constexpr uint32_t OOB = 0x80000000u;
 
 __host__ __device__ constexpr int swz(int img) { return (0x1320 >> (4 * img)) & 3; }
 
+// Patch geometry of stride S: rows S*TH + 3 - S, columns 6 (S = 1) or 9 (S = 2, input columns 2x0 - 1 ..
+// 2x0 + 7, stored even columns first: slot c / 2 for even c, 5 + c / 2 for odd c, so the four lanes'
+// columns 2x + s of every tap are four consecutive slots, as with S = 1).
+template <int S> __host__ __device__ constexpr int patch_cols() { return S == 1 ? FC + 2 : 2 * FC + 1; }
+template <int S> __host__ __device__ constexpr int col_slot(int c) { return S == 1 ? c : ((c & 1) ? 5 + (c >> 1) : (c >> 1)); }
+
 // WM x WN waves; wave (wm, wn) owns output rows wm*TM .. wm*TM+TM-1 of the tile and channels
-// n0 + wn*TN*16 .. +TN*16; PD = weight prefetch distance in column steps (3 per chunk).  Images past B
+// n0 + wn*TN*16 .. +TN*16; PD = weight prefetch distance in column steps (3 per chunk); S = stride
+// (2: tap (r, s) of output (y, x) is input (2y - 1 + r, 2x - 1 + s): a wave reads patch rows
+// 2*wm*TM .. 2*wm*TM + 2*TM once per column step, output row i taking rows 2i + r).  Images past B
 // (B not a multiple of 4) read zeros (past the input's buffer range) and store nothing.
-template <int WM, int WN, int TN, int TM, int NCH, int ACT, int PD>
+template <int WM, int WN, int TN, int TM, int NCH, int ACT, int PD, int S>
 __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) : 1) void conv3x3_lr_kernel(const ConvParams p) {
   constexpr int NT = 64 * WM * WN;
-  constexpr int TH = TM * WM, PR = TH + 2;
+  constexpr int TH = TM * WM, PR = S * TH + 3 - S, PC = patch_cols<S>();
+  constexpr int NXA = S * TM + 3 - S;            // patch rows a wave reads per column step
   constexpr int PPX = FI * PR * PC;              // patch pixels
   constexpr int PB = PPX * 64;                   // bytes per patch buffer
   constexpr int BN = WN * TN * 16;
@@ -67,10 +75,10 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
   const int nN = (p.cout + BN - 1) / BN;
   const int nt = t % nN;
   t /= nN;
-  const int ncg = p.W / FC;
+  const int ncg = p.Wo / FC;
   const int x0 = (t % ncg) * FC;
   t /= ncg;
-  const int nrg = p.H / TH;   // (t / nrg: image group, ceil(B / 4) of them)
+  const int nrg = p.Ho / TH;   // (t / nrg: image group, ceil(B / 4) of them)
   const int y0 = (t % nrg) * TH;
   const int b0 = (t / nrg) * FI;
   const int n0 = nt * BN;
@@ -88,8 +96,8 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
     if (px < PPX) {
       const int img = px / (PR * PC), r2 = px - img * (PR * PC);
       const int row = r2 / PC, col = r2 - row * PC;
-      po[k] = (uint32_t)((pix_index(b0 + img, y0 - 1 + row, x0 - 1 + col, p.H, p.W) * p.xc + p.xoff + qq * 8) * 2);
-      pd[k] = (uint32_t)(px * 64 + ((qq ^ swz(img)) * 16));
+      po[k] = (uint32_t)((pix_index(b0 + img, S * y0 - 1 + row, S * x0 - 1 + col, p.H, p.W) * p.xc + p.xoff + qq * 8) * 2);
+      pd[k] = (uint32_t)(((img * PR + row) * PC + col_slot<S>(col)) * 64 + ((qq ^ swz(img)) * 16));
     } else {
       po[k] = OOB;
       pd[k] = 0xffffffffu;
@@ -136,7 +144,7 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
   // per-lane patch read offset: image li / 4, column li % 4 (+ s), slot g ^ f(image)
   const int img = li >> 2;
   const uint32_t a_lane = (uint32_t)(((img * PR) * PC + (li & 3)) * 64 + ((g ^ swz(img)) * 16));
-  const uint32_t a_wave = (uint32_t)(wm * TM * PC * 64);
+  const uint32_t a_wave = (uint32_t)(S * wm * TM * PC * 64);
 
   // ---- prologue: chunk 0's patch into buffer 0, chunk 1's in registers, PD phases of weights
   load_patch(0);
@@ -153,10 +161,11 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
     for (int s = 0; s < 3; ++s) {
       const int ph = c * 3 + s;
       if (ph + PD < NPH) load_w(ph + PD, wreg[(ph + PD) % NWB]);
-      const unsigned char* pb = smem + (c & 1) * PB + a_wave + a_lane + s * 64;
-      u4 xa[TM + 2];
+      // the lane's column 2x + s (S = 2) or x + s sits in slot x + col_slot(s) - col_slot(0)
+      const unsigned char* pb = smem + (c & 1) * PB + a_wave + a_lane + col_slot<S>(s) * 64;
+      u4 xa[NXA];
 #pragma unroll
-      for (int j = 0; j < TM + 2; ++j) xa[j] = *reinterpret_cast<const u4*>(pb + j * PC * 64);
+      for (int j = 0; j < NXA; ++j) xa[j] = *reinterpret_cast<const u4*>(pb + j * PC * 64);
       const u4(&w)[3][TN] = wreg[ph % NWB];
 #pragma unroll
       for (int r = 0; r < 3; ++r)
@@ -165,7 +174,7 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
 #pragma unroll
           for (int i = 0; i < TM; ++i)
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w[r][j]),
-                                                               __builtin_bit_cast(h8, xa[i + r]), acc[j][i], 0, 0, 0);
+                                                               __builtin_bit_cast(h8, xa[S * i + r]), acc[j][i], 0, 0, 0);
     }
     if (c + 1 < NCH) {
       store_patch((c + 1) & 1);   // buffer of chunk c - 1: every wave left it at the last barrier
@@ -231,36 +240,43 @@ __global__ void pack_frag3x3_kernel(const _Float16* w, int kpad, int cin, int nf
   }
 }
 
-template <int WM, int WN, int TN, int TM, int PD, int NCH>
+template <int WM, int WN, int TN, int TM, int PD, int S, int NCH>
 hipError_t launch_cfg(const ConvParams& p, hipStream_t st) {
   constexpr int TH = TM * WM, BN = WN * TN * 16;
-  const long T = (long)((p.B + FI - 1) / FI) * (p.H / TH) * (p.W / FC) * ((p.cout + BN - 1) / BN);
-  if (p.act == 1) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 1, PD>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
-  else if (p.act == 2) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 2, PD>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
-  else YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 0, PD>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
+  const long T = (long)((p.B + FI - 1) / FI) * (p.Ho / TH) * (p.Wo / FC) * ((p.cout + BN - 1) / BN);
+  if (p.act == 1) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 1, PD, S>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
+  else if (p.act == 2) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 2, PD, S>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
+  else YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 0, PD, S>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
   return hipGetLastError();
 }
 
-template <int WM, int WN, int TN, int TM, int PD>
+template <int WM, int WN, int TN, int TM, int PD, int S>
 hipError_t launch_nch(const ConvParams& p, hipStream_t st) {
   switch (p.cin / CK) {
-    case 2: return launch_cfg<WM, WN, TN, TM, PD, 2>(p, st);
-    case 4: return launch_cfg<WM, WN, TN, TM, PD, 4>(p, st);
-    case 8: return launch_cfg<WM, WN, TN, TM, PD, 8>(p, st);
-    case 16: return launch_cfg<WM, WN, TN, TM, PD, 16>(p, st);
+    case 2: return launch_cfg<WM, WN, TN, TM, PD, S, 2>(p, st);
+    case 4: return launch_cfg<WM, WN, TN, TM, PD, S, 4>(p, st);
+    case 6: return launch_cfg<WM, WN, TN, TM, PD, S, 6>(p, st);
+    case 8: return launch_cfg<WM, WN, TN, TM, PD, S, 8>(p, st);
+    case 12: return launch_cfg<WM, WN, TN, TM, PD, S, 12>(p, st);
+    case 16: return launch_cfg<WM, WN, TN, TM, PD, S, 16>(p, st);
+    case 24: return launch_cfg<WM, WN, TN, TM, PD, S, 24>(p, st);
   }
   return hipErrorInvalidValue;
 }
 
-// tile configurations {WM, WN, TN, TM, PD} (variants 270 + row): pixels 16 * WM * TM x channels
-// 16 * WN * TN, weights PD column steps ahead.  Kept from the round-4 sweep of 20 configurations
-// (profiles/r4lr/tune{1,2,3}.txt, one layer forced at a time in the yolov7 bs-32 forward): 4-wave blocks
-// of 80-pixel tiles with the weights three column steps ahead won every layer shape; the 8-wave and
-// 128 / 160-pixel tiles, and two steps of prefetch, lost by 5-20 %.  0: 80 x 128, 1: 80 x 64; 2 / 3:
-// the same with 64-pixel tiles for heights that 5 does not divide.
-#define LR_CFGS(X) X(0, 1, 4, 2, 5, 3) X(1, 1, 4, 1, 5, 3) X(2, 1, 4, 2, 4, 3) X(3, 1, 4, 1, 4, 3)
-#define LR_ROW(i, wm, wn, tn, tm, pd) {wm, wn, tn, tm, pd},
-constexpr int LR_CFG[][5] = {LR_CFGS(LR_ROW)};
+// tile configurations {WM, WN, TN, TM, PD, S} (variants 270 + row): pixels 16 * WM * TM x channels
+// 16 * WN * TN, weights PD column steps ahead, stride S.  Kept from the round-4 sweep of 20 stride-1
+// configurations (profiles/r4lr/tune{1,2,3}.txt, one layer forced at a time in the yolov7 bs-32
+// forward): 4-wave blocks of 80-pixel tiles with the weights three column steps ahead won every layer
+// shape; the 8-wave and 128 / 160-pixel tiles, and two steps of prefetch, lost by 5-20 %.  0: 80 x 128,
+// 1: 80 x 64; 2 / 3: the same with 64-pixel tiles for heights that 5 does not divide.  The same four at
+// stride 2 were correct but slower than the dispatch on five of the six yolov7 stride-2 layers
+// (profiles/r4lr/convbench_s2.txt: 64->128 s2 @320 243 vs 215 us, 256->256 s2 @80 77 vs 68; a 9-column,
+// 2*TH+1-row patch per 80 outputs is 4.9 input pixels per output against 2.1 at stride 1), so none is
+// instantiated; the kernel keeps S as a parameter.
+#define LR_CFGS(X) X(0, 1, 4, 2, 5, 3, 1) X(1, 1, 4, 1, 5, 3, 1) X(2, 1, 4, 2, 4, 3, 1) X(3, 1, 4, 1, 4, 3, 1)
+#define LR_ROW(i, wm, wn, tn, tm, pd, s) {wm, wn, tn, tm, pd, s},
+constexpr int LR_CFG[][6] = {LR_CFGS(LR_ROW)};
 constexpr int LR_NCFG = sizeof(LR_CFG) / sizeof(LR_CFG[0]);
 
 }  // namespace
@@ -278,19 +294,20 @@ hipError_t pack_frag3x3(const void* w, int kpad, int cin, int cout, void* out, h
 // cfg: LR_CFG row (variants 270 + cfg)
 bool lr_supported(const ConvParams& p, int cfg) {
   if (cfg < 0 || cfg >= LR_NCFG) return false;
-  const int th = LR_CFG[cfg][0] * LR_CFG[cfg][3];
+  const int th = LR_CFG[cfg][0] * LR_CFG[cfg][3], S = LR_CFG[cfg][5];
   const int nch = p.cin / CK;
-  return p.wf && p.k == 3 && p.s == 1 && p.pad == 1 && !p.pool && p.cin % CK == 0 &&
-         (nch == 2 || nch == 4 || nch == 8 || nch == 16) && p.cout % 16 == 0 && p.cout <= 1024 && p.Ho == p.H &&
-         p.Wo == p.W && p.H % th == 0 && p.W % FC == 0 && p.xoff % 8 == 0 && p.xc % 8 == 0 && p.yoff % 8 == 0 &&
+  const bool geom = S == 1 ? (p.Ho == p.H && p.Wo == p.W) : (p.H % 2 == 0 && p.W % 2 == 0 && p.Ho == p.H / 2 && p.Wo == p.W / 2);
+  return p.wf && p.k == 3 && p.s == S && p.pad == 1 && !p.pool && p.cin % CK == 0 && geom &&
+         (nch == 2 || nch == 4 || nch == 6 || nch == 8 || nch == 12 || nch == 16 || nch == 24) && p.cout % 16 == 0 &&
+         p.cout <= 1024 && p.Ho % th == 0 && p.Wo % FC == 0 && p.xoff % 8 == 0 && p.xc % 8 == 0 && p.yoff % 8 == 0 &&
          p.yc % 8 == 0;
 }
 
 hipError_t launch_conv_lr(const ConvParams& p, int cfg, hipStream_t st) {
   if (!lr_supported(p, cfg)) return hipErrorInvalidValue;
   switch (cfg) {
-#define LR_CASE(i, wm, wn, tn, tm, pd) \
-  case i: return launch_nch<wm, wn, tn, tm, pd>(p, st);
+#define LR_CASE(i, wm, wn, tn, tm, pd, s) \
+  case i: return launch_nch<wm, wn, tn, tm, pd, s>(p, st);
     LR_CFGS(LR_CASE)
 #undef LR_CASE
   }
