@@ -114,9 +114,21 @@ def plumbing(a):
         model = Model(a.model)
         synthetic_state_dict(model, seed=0)
         model = model.float().fuse().eval()
-    g = compile_model(model, L.DT_F16)
-    blob = ydist.broadcast_blob(g, torch.device('cpu'))
-    same = torch.equal(blob, g.weight_blob())
+    if a.dtype == 'fp8':
+        # the fp8 plan's path: rank 0's activation scales, then its packed blob.  Calibration needs the GPU,
+        # so rank 0 stands in seeded power-of-two scales here; the other ranks must end with its scales
+        # and a blob identical to the one rank 0 packed from them.
+        from yv7.graph import FP8_MIN_COUT, fp8_candidates
+        mc = FP8_MIN_COUT if a.fp8_min_cout is None else a.fp8_min_cout
+        ops = fp8_candidates(compile_model(model, L.DT_F16), mc)
+        stand_in = {i: 2.0 ** -((i * 7) % 5) for i in ops} if rank == 0 else None
+        _, g, blob = ydist.broadcast_fp8_plan(model, torch.device('cpu'), min_cout=mc, scales=stand_in)
+        ref = compile_model(model, L.DT_F16, fp8={i: 2.0 ** -((i * 7) % 5) for i in ops})
+        same = len(ops) > 0 and torch.equal(blob, ref.weight_blob())
+    else:
+        g = compile_model(model, L.DT_F16)
+        blob = ydist.broadcast_blob(g, torch.device('cpu'))
+        same = torch.equal(blob, g.weight_blob())
     lo, hi = ydist.shard(a.batch * world, rank, world)
     b = hi - lo
     det = torch.full((b, 300, 6), float(rank))
@@ -136,7 +148,7 @@ def plumbing(a):
     pl = [torch.zeros_like(per) for _ in range(world)]
     dist.all_gather(pl, per)
     if rank == 0:
-        print(json.dumps({'plumbing': True, 'n_gpus': world, 'world_size_seen': world, 'backend': 'gloo',
+        print(json.dumps({'plumbing': True, 'dtype': a.dtype, 'n_gpus': world, 'world_size_seen': world, 'backend': 'gloo',
                           'weights_broadcast_bytes': int(blob.numel()), 'global_batch': a.batch * world,
                           'all_ranks_ok': bool(flags.item()),
                           'allgather_us_per_batch': [round(float(v[0]), 1) for v in pl],
@@ -276,7 +288,9 @@ def main(argv=None):
         model = Model(a.model)
         synthetic_state_dict(model, seed=0)
         model = model.float().fuse().eval()
-    if a.dtype == 'fp8':   # every rank calibrates its own fp8 plan (deterministic: same frames, same scales)
+    if a.dtype == 'fp8' and distributed:   # rank 0 calibrates, every rank gets its scales and packed blob
+        plan = ydist.broadcast_fp8_plan(model, dev, min_cout=a.fp8_min_cout)[0]
+    elif a.dtype == 'fp8':
         plan = Plan.fp8_from_model(model, dev, min_cout=a.fp8_min_cout)
     elif distributed:
         plan = ydist.broadcast_weights(model, dev, dt)

@@ -10,6 +10,7 @@
 #   tune=OPS:CANDS[:ROUNDS]     tune_ops.py: each candidate forced on one op at a time -> tune.txt
 #                               (OPS = all for every conv op)
 #   bench[=N][@ENV=V,...]       N bench lines (default 2), --steps 40 --warmup 5  -> bench_STEP_I.json
+#   dispatch[=NAME]             scripts/dump_dispatch.py (default dispatch of the 3 bench plans) -> dispatch_NAME.txt
 #   lib=NAME                    run the following steps on yolo-series_amd/yv7/libyv7_NAME.so (an
 #                               A/B baseline built elsewhere); lib=cur restores the tree's library
 # e.g. bash scripts/gpu_steps.sh r4a tests ops=base ops=nodual@YV7_DUAL=0 tune=8,12:239,234:3 bench=2
@@ -61,6 +62,10 @@ for step in "$@"; do
           > $f 2> ${f%.json}.err || exit 1
         python -c "import json;d=json.load(open('$f'));print('bench', '$f', '$envs', d['value'], d['detail']['serial_forward_ms'])"
       done ;;
+    dispatch)
+      timeout -k 10 300 python -u scripts/dump_dispatch.py $O/dispatch_${arg:-cur}.txt > $O/dispatch_${arg:-cur}.log 2>&1 \
+        || { tail $O/dispatch_${arg:-cur}.log; exit 1; }
+      tail -1 $O/dispatch_${arg:-cur}.log ;;
     lib)
       [ -f $LIBD/libyv7_cur.so ] || cp $LIBD/libyv7.so $LIBD/libyv7_cur.so
       cp $LIBD/libyv7_$arg.so $LIBD/libyv7.so || exit 1 ;;

@@ -22,7 +22,7 @@ from yv7.runtime import Plan  # noqa: E402
 from yv7.synthetic import synthetic_state_dict  # noqa: E402
 
 RING = [100 + 10 * c + s for c in range(6) for s in (0, 2, 4)]
-DEFAULT_CANDS = [201, 202, 203, 204, 205, 206, 217, 221, 222, 223, 4, 5, 6, 7, 8] + RING
+DEFAULT_CANDS = [201, 202, 203, 204, 205, 206, 231, 232, 262, 270, 271, 4, 5, 6, 7, 8] + RING
 
 ap = argparse.ArgumentParser()
 ap.add_argument('--model', default='yolov7')

@@ -121,6 +121,113 @@ def test_gloo_world2_inflight_gather_order():
             assert c == list(range(h * 6, h * 6 + 6)), (rank, h, c)
 
 
+def _uneven_drain_worker(rank, world, port, q):
+    """Rank 0 collects every batch right after submitting it (nothing in flight at the end); rank 1 keeps
+    S batches in flight and drains the last ones newest-first.  The all-gather is issued inside
+    submit(), in submission order, on both ranks, so the ranks' different collection orders cannot
+    mis-pair or deadlock the collectives."""
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, 'yolo-series_amd'), root]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from yv7.dist import gather_detections
+        from yv7.runtime import Inflight
+        B, S, nb = 3, 3, 8
+        run = Inflight(_HostPlan(), B, 2, 2, streams=S, max_det=5, post=gather_detections, nms=_host_nms)
+        got = {}
+        for h in range(nb):
+            x = torch.zeros(B, 3, 2, 2)
+            x[:, 0, 0, 0] = torch.arange(B) + h * B * world + rank * B
+            assert run.submit(x) == h
+            if rank == 0:
+                got[h] = run.result(h)[2].tolist()
+            elif h >= S - 1 and h % 2 == 0:
+                got[h - S + 1] = run.result(h - S + 1)[2].tolist()
+        for j in reversed(range(nb - S, nb)):   # rank 1: the batches still in flight, newest first
+            if j not in got:
+                got[j] = run.result(j)[2].tolist()
+        run.close()
+        q.put((rank, got))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_inflight_uneven_drain():
+    """two ranks with different numbers of batches in flight when they stop
+    submitting (0 on rank 0, S on rank 1) and different collection orders: every batch either rank
+    collected is that batch's detections of the whole global batch, in global image order."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uneven_drain_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, got in res:
+        assert got, rank
+        for h, c in got.items():
+            assert c == list(range(h * 6, h * 6 + 6)), (rank, h, c)
+    assert sorted(dict(res)[0]) == list(range(8))
+
+
+def _uneven_shard_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, 'yolo-series_amd'), root]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        sizes = [hi - lo for lo, hi in (shard(7, r, world) for r in range(world))]
+        lo, hi = shard(7, rank, world)
+        b = hi - lo
+        det = torch.arange(lo, hi, dtype=torch.float32).view(b, 1, 1).expand(b, 300, 6).contiguous()
+        src = torch.arange(lo, hi, dtype=torch.int64).view(b, 1).expand(b, 300).contiguous()
+        cnt = torch.arange(lo, hi, dtype=torch.int32)
+        gd, gs, gc = gather_detections(det, src, cnt, sizes=sizes)
+        q.put((rank, gd[:, 0, 0].tolist(), gs[:, 0].tolist(), gc.tolist()))
+    finally:
+        dist.destroy_process_group()
+
+
+def test_gloo_world2_uneven_shard_gather():
+    """A global batch that the ranks cannot split evenly (7 over 2: 4 + 3): the gather pads to the
+    largest shard and returns exactly the 7 images in order."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_uneven_shard_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=300) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    for rank, d, s_, c in res:
+        assert d == list(range(7)) and s_ == list(range(7)) and c == list(range(7)), rank
+
+
+def test_bench_plumbing_fp8():
+    """`bench.py --gpus 2 --plumbing --dtype fp8`: rank 0's fp8 activation scales and packed blob reach
+    rank 1 (yv7.dist.broadcast_fp8_plan), one JSON line."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')}
+    out = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '2', '--plumbing', '--dtype', 'fp8',
+                          '--model', 'yolov7-tiny', '--batch', '2'], capture_output=True, text=True, env=env,
+                         timeout=600)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, out.stdout
+    assert lines[0]['dtype'] == 'fp8' and lines[0]['all_ranks_ok'] and lines[0]['per_rank_world_size_seen'] == [2, 2]
+
+
 def test_shard_partition():
     for B, W in [(256, 8), (32, 1), (10, 4), (3, 4)]:
         parts = [shard(B, r, W) for r in range(W)]
@@ -201,3 +308,29 @@ def test_rccl_world1_broadcast_gather_inflight():
         run.close()
     finally:
         dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+def test_rccl_world1_fp8_broadcast():
+    """The fp8 plan's multi-GPU creation on the real backend (world size 1): rank 0 calibrates, the scales
+    and the packed blob are RCCL-broadcast (yv7.dist.broadcast_fp8_plan) — the blob and the forward equal
+    Plan.fp8_from_model's (what every rank computed for itself before round 4)."""
+    from helpers import fresh_model, frames
+    from yv7.dist import broadcast_fp8_plan
+    from yv7.runtime import Plan
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(_free_port()))
+    dev = torch.device('cuda:0')
+    torch.cuda.set_device(dev)
+    dist.init_process_group('nccl', rank=0, world_size=1, device_id=dev)
+    try:
+        m = fresh_model('yolov7-tiny')
+        plan, g, blob = broadcast_fp8_plan(m, dev)
+        ref = Plan.fp8_from_model(m, dev)
+        assert torch.equal(blob.cpu(), ref.graph.weight_blob())
+        x = frames(2, 256, 256, seed=5).to(dev).half()
+        za, _ = plan.forward(x, want_raw=False)
+        zb, _ = ref.forward(x, want_raw=False)
+        assert torch.equal(za, zb)
+    finally:
+        dist.destroy_process_group()
+

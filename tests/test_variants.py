@@ -7,8 +7,10 @@ a small frame exercises only some of them; forcing each one on every layer shape
 yolov7-tiny covers them all: the generic tile kernels (1, 2, 8), the 8-wave LDS-DMA rings (4-7),
 the halo and weight-stationary 3x3 kernels (10, 11, and 15: its half-patch ring form), every ring configuration with 1, 2 and 4 K
 splits (1CS: configuration C, S splits; the split-K hand-off of splitk_reduce), the persistent rings
-(201-206, BK 32: 211-218), the pipelined persistent rings (221-223), the 8-phase rings (231-233), the weight-stationary 1x1 rings (234-236, and 239: N-split), the stream-K 8-phase ring (237), the 512x128 8-phase ring (238), the register-streamed 1x1 (240), the 3x3 halo rings (260: 128-channel tiles, 261: 256-channel tiles, 262: column-group form), the
-low-resolution 3x3 kernel (270-273: 80 / 64-pixel tiles of 4 images x 4 columns, 128 / 64 channels) and
+(201-206), the 8-phase rings (231: 256 x 256, 232: 256 x 128), the weight-stationary 1x1 rings (234-236,
+and 239: N-split), the column-group 3x3 halo ring (262), the
+low-resolution 3x3 kernel (270-273: 80 / 64-pixel tiles of 4 images x 4 columns, 128 / 64 channels;
+274: stride 2) and
 the alternative Detect heads (92, 97, and 99: the 64 x 256 ring that was the default before the
 persistent head).  A variant a layer's shape
 does not support falls back to the tuned kernel, which the check then covers again.
@@ -26,8 +28,7 @@ DEV = 'cuda:0'
 
 CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15,
                  100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
-                 201, 202, 203, 204, 205, 206, 211, 212, 213, 214, 215, 216, 217, 218, 221, 222, 223, 231, 232, 233, 234, 235, 236, 237, 238, 239, 240,
-                 260, 261, 262, 270, 271, 272, 273]
+                 201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274]
 DET_VARIANTS = [92, 97, 99]
 
 
@@ -65,7 +66,8 @@ def test_variant_api_rejects_hooks():
     m = fresh_model('yolov7-tiny').to(DEV).half()
     plan = m.plan()
     conv = next(i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV)
-    for v in (12, 13, 14, 16, 17, 18, 19, 90, 91, 93, 94, 298, 160, 105, 241, 248, 255, 259, 263):
+    for v in (12, 13, 14, 16, 17, 18, 19, 90, 91, 93, 94, 298, 160, 105, 211, 221, 233, 237, 238, 240, 241,
+              248, 255, 259, 260, 261, 263, 275, 911):
         with pytest.raises(RuntimeError):
             plan.set_op_variant(conv, v)
     with pytest.raises(RuntimeError):

@@ -1338,199 +1338,6 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * BK * 2 <= 48 * 
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-// s_waitcnt immediate (gfx9 family encoding): vmcnt(vm) expcnt(none) lgkmcnt(0)
-constexpr int waitcnt_vm_lgkm0(int vm) { return (vm & 15) | (7 << 4) | (((vm >> 4) & 3) << 14); }
-
-// ---------------------------------------------------------------------------------------------
-// Pipelined persistent ring.  The persistent ring above reads both 32-deep fragment sets of a K step
-// right after its barrier and only then issues the MFMAs, and its barrier puts the two waves of a
-// SIMD in phase every step: both read, the matrix pipe idles, both multiply.  Here each wave keeps
-// two fragment register sets and the step is split around the barrier:
-//     reads F1(k)            (LDS stage k, 2nd 32-deep half)  |  MFMA F0(k)
-//     lgkmcnt(0) + vmcnt(stage k+1 landed) + s_barrier
-//     DMA stage k+2 into stage k's slot (every wave is done reading stage k)
-//     reads F0(k+1)          (stage k+1, 1st half)            |  MFMA F1(k) [+ tile epilogue]
-// so every fragment read is in flight under the wave's own previous MFMA cluster.  Two LDS stages of
-// BK = 64; a stage's DMA has one K step of MFMAs to land (as in the ring above).  The tile walk, the
-// DMA addressing and the register epilogue are the persistent ring's.
-template <int BM, int BN, int WM, int WN, bool ONE, int ACT>
-__global__ __launch_bounds__(64 * WM * WN, (2 * (BM + BN) * 128 <= 76 * 1024) ? 2 : 1) void conv_f16_pp_kernel(
-    const ConvParams p) {
-  constexpr int BK = 64, STAGES = 2;
-  constexpr int NW = WM * WN, NTH = 64 * NW;
-  constexpr int WTM = BM / WM, WTN = BN / WN;
-  constexpr int TM = WTM / 16, TN = WTN / 16;
-  constexpr int RB_ = BK * 2;              // LDS bytes per tile row
-  constexpr int RPI = 8;                   // tile rows per DMA wave-instruction (1 KiB)
-  constexpr int RA = BM / RPI / NW, RB = BN / RPI / NW;
-  static_assert(RA * RPI * NW == BM && RB * RPI * NW == BN, "tile rows must split into DMA groups per wave");
-  static_assert(TN % 2 == 0, "the epilogue pairs 16-channel groups");
-  constexpr int NST = TM * TN / 2;         // epilogue stores per lane per tile
-  constexpr int STAGE = (BM + BN) * RB_;
-  constexpr int BIAS = 4096;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[STAGES * STAGE + BIAS];
-  float* bias_l = reinterpret_cast<float*>(smem + STAGES * STAGE);
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
-  const int wm = wave / WN, wn = wave % WN;
-  const int g = lane >> 4, li = lane & 15;
-  const int lr = lane >> 3;
-  const int c = swz_bk<BK>(lr, lane & 7);
-
-  const int nN = (p.cout + BN - 1) / BN;
-  const int T = ((p.M + BM - 1) / BM) * nN;
-  const int G = gridDim.x;
-  const int nk = p.kpad / BK;
-  const int ntl = (T - (int)blockIdx.x + G - 1) / G;
-  const int nsteps = ntl * nk;
-
-  const auto xr = make_rsrc(p.x, p.xbytes);
-  const auto wr = make_rsrc(p.w, p.wbytes);
-  const auto yr = make_rsrc(p.y, 0x7fffffffu);
-
-  for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
-
-  AWalk<ONE, RA, BK> aw;
-  uint32_t b_off0 = 0;   // weight row of group j: b_off0 + j * bstride (one VGPR instead of RB)
-  const uint32_t bstride = (uint32_t)(NW * RPI * p.kpad * 2);
-  int ig = 0, it = 0, ikt = 0;
-  auto issue_next = [&]() {
-    if (ikt == 0) {
-      const int t = blockIdx.x + it * G;
-      const int m0 = (t / nN) * BM, n0 = (t % nN) * BN;
-      aw.init(p, c, 0);
-      PixelWalk pw(p, m0 + wave * RPI + lr);
-#pragma unroll
-      for (int j = 0; j < RA; ++j) {
-        if (j) pw.advance(p, NW * RPI);
-        aw.off[j] = a_origin(p, pw.b, pw.ho, pw.wo, c);
-      }
-      b_off0 = (uint32_t)(((n0 + wave * RPI + lr) * p.kpad + c * 8) * 2);
-    }
-    unsigned char* As = smem + (ig & 1) * STAGE;
-    unsigned char* Bs = As + BM * RB_;
-    aw.step(p, ikt, [&](int j, uint32_t vo, uint32_t so) { dma16(xr, As + (j * NW + wave) * RPI * RB_, vo, so); });
-#pragma unroll
-    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * RPI * RB_, b_off0 + j * bstride, (uint32_t)ikt * BK * 2);
-    ++ig;
-    if (++ikt == nk) { ikt = 0; ++it; }
-  };
-
-  f4 acc[TN][TM];
-  int cm0 = 0, cn0 = 0;
-  auto init_tile = [&](int i) {
-    const int t = blockIdx.x + i * G;
-    cm0 = (t / nN) * BM;
-    cn0 = (t % nN) * BN;
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = cn0 + wn * WTN + j * 16 + g * 4;
-      f4 bv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? bias_l[col + e] : 0.0f;
-#pragma unroll
-      for (int ii = 0; ii < TM; ++ii) acc[j][ii] = bv;
-    }
-  };
-  const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
-  auto epilogue = [&]() {
-    PixelWalk pw(p, cm0 + wm * WTM + li);
-#pragma unroll
-    for (int ii = 0; ii < TM; ++ii) {
-      if (ii) pw.advance(p, 16);
-      const int m = cm0 + wm * WTM + ii * 16 + li;
-      const uint32_t yo = (uint32_t)((pix_index(pw.b, pw.ho, pw.wo, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
-#pragma unroll
-      for (int mp = 0; mp < TN / 2; ++mp) {
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-        h4 va, vb;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          va[e] = (_Float16)act_t<ACT>(acc[2 * mp][ii][e]);
-          vb[e] = (_Float16)act_t<ACT>(acc[2 * mp + 1][ii][e]);
-        }
-        const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
-        const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
-        const u4 v = {s0[0], s1[0], s0[1], s1[1]};
-        const int n = cn0 + wn * WTN + mp * 32 + (int)lane_ch;
-        const uint32_t off = (m < p.M && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu;
-        __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
-      }
-    }
-  };
-
-  // fragment sets: F0 = K elements [0, 32) of a stage, F1 = [32, 64)
-  u4 xa0[TM], wb0[TN], xa1[TM], wb1[TN];
-  auto read_frag = [&](int slot, int sb, u4 (&xa)[TM], u4 (&wb)[TN]) {
-    const unsigned char* As = smem + slot * STAGE;
-    const unsigned char* Bs = As + BM * RB_;
-    const int ch = sb * 4 + g;
-#pragma unroll
-    for (int ii = 0; ii < TM; ++ii) {
-      const int row = wm * WTM + ii * 16 + li;
-      xa[ii] = *reinterpret_cast<const u4*>(As + row * RB_ + swz_bk<BK>(row, ch) * 16);
-    }
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int row = wn * WTN + j * 16 + li;
-      wb[j] = *reinterpret_cast<const u4*>(Bs + row * RB_ + swz_bk<BK>(row, ch) * 16);
-    }
-  };
-  auto mfma = [&](const u4 (&xa)[TM], const u4 (&wb)[TN]) {
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int ii = 0; ii < TM; ++ii)
-        acc[j][ii] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]), __builtin_bit_cast(h8, xa[ii]),
-                                                            acc[j][ii], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-  };
-
-  issue_next();
-  if (nsteps > 1) issue_next();
-  if (nsteps > 1) asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(RA + RB) : "memory");
-  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  init_tile(0);
-  read_frag(0, 0, xa0, wb0);
-
-  int ci = 0, ckt = 0;
-  bool stores_pending = false;   // the previous step ended a tile: its NST stores are younger than stage gs+1
-  for (int gs = 0; gs < nsteps; ++gs) {
-    const int slot = gs & 1;
-    read_frag(slot, 1, xa1, wb1);
-    mfma(xa0, wb0);
-    __builtin_amdgcn_sched_barrier(0);
-    // F1(gs) reads done (so the whole stage gs has been read by this wave) and stage gs+1 landed.
-    // The builtin (not inline asm), on every path, lets the compiler's own wait insertion see that the
-    // F1 reads are retired, so it does not hold F1's MFMAs back for the F0(gs+1) reads issued below.
-    if (stores_pending) __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(NST));
-    else __builtin_amdgcn_s_waitcnt(waitcnt_vm_lgkm0(0));
-    if (gs + 1 < nsteps) {
-      __builtin_amdgcn_s_barrier();
-      __builtin_amdgcn_sched_barrier(0);
-      if (ig < nsteps) issue_next();   // stage gs+2 -> slot gs & 1
-    }
-    // F0(gs+1) (after the last step a harmless read of the other slot): issued on every path, so the
-    // compiler's wait insertion (which does not credit the wait above) sees the same read sequence
-    // ahead of F1's MFMAs on every path and counts only the F0 reads as younger
-    read_frag(slot ^ 1, 0, xa0, wb0);
-    mfma(xa1, wb1);
-    stores_pending = false;
-    if (++ckt == nk) {
-      epilogue();
-      stores_pending = true;
-      ckt = 0;
-      if (++ci < ntl) init_tile(ci);
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // ---------------------------------------------------------------------------------------------
 // 8-phase persistent ring (256 x 256 tiles, 8 waves = 2 stagger groups x 4, BK 64): the structure of
 // the guide's 256^2 "8-phase" GEMM template (cdna_hip_programming.md §5: counted vmcnt across raw
@@ -1553,11 +1360,10 @@ __global__ __launch_bounds__(64 * WM * WN, (2 * (BM + BN) * 128 <= 76 * 1024) ? 
 //  * the finished tile's epilogue (bias in the accumulators, activation, fp16, permlane16 pairing,
 //    16-byte NHWC stores) runs between the last K-tile's phase 3 and the next tile's phase 0.
 // acc[hb][j][ha][i] = channels hb*128 + wn*32 + j*16 + g*4 + e of pixel ha*128 + wm*64 + i*16 + li.
-// OPT (experiments, variants 240 + OPT): 1 = DMA issued before the phase's LDS reads, 2 = no s_setprio,
-// 4 = XCD-major persistent tile order, 8 = only group 1 retires its reads before the first barrier
-// BM x BN = 256 x 256 (wide layers) or 512 x 128 (128-channel layers: the same 128 x 64 output per
-// wave and 16 MFMAs per phase; A halves of 256 rows, B halves of 64, bias read from global).
-template <bool ONE, int ACT, int OPT = 0, int BM = 256, int BN = 256>
+// Persistent tile order: XCD-major (xcd_tile_walk; 1x1 1024->1024 @40 140 -> 133 us, tune_ops).  The
+// round-2 schedule experiments (DMA before the reads, no s_setprio, one group retiring early, B half 0
+// kept in registers, stream-K, 512 x 128 tiles: DESIGN §4.5, §8) were removed in round 4.
+template <bool ONE, int ACT, int BM = 256, int BN = 256>
 __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p) {
   constexpr int NTH = 512;
   constexpr int AHR = BM / 2, BHR = BN / 2;          // rows per A / B half-tile
@@ -1568,8 +1374,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   constexpr int WNC = BHR / 32;                      // waves across a B half (32 channels each)
   static_assert(AP >= 1 && BP >= 1 && (AHR / 64) * WNC == 8, "8 waves of 64 x 32 per block quadrant");
   constexpr int BIASB = (2 * BUF + 4096 + 16 <= 163840) ? 4096 : 0;   // bias in LDS when it fits
-  constexpr bool SK = (OPT & 32) != 0;               // stream-K: even K-tile ranges over the grid
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + BIASB + (SK ? 16 : 0)];
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * BUF + BIASB];
   float* bias_l = reinterpret_cast<float*>(smem + 2 * BUF);
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1582,21 +1387,12 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
 
   const int nN = (p.cout + BN - 1) / BN;
   const int T = ((p.M + BM - 1) / BM) * nN;
-  const int G = gridDim.x;
   const int nk = p.kpad / BKE;
-  // persistent tile order: XCD-major (OPT 4, xcd_tile_walk), else tiles blockIdx, + G, ...
-  const TileWalk tw = (OPT & 4) ? xcd_tile_walk(T) : TileWalk{(int)blockIdx.x, G, T};
-  int ntl = tw.count();
-  int total = ntl * nk;                              // K-tiles this block computes
-  // stream-K (OPT 32): the T*nk K-tiles of the layer, tile-major, split evenly over the G blocks (XCD-
-  // major virtual order, so a tile's blocks are neighbours); tiles cut between blocks are finished by
-  // their last-arriving block from the others' fp32 partials (handoff below)
-  const long TK = (long)T * nk;
-  const int vbk = G % 8 == 0 ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
-  const int g0 = SK ? (int)(vbk * TK / G) : 0;
-  if constexpr (SK) total = (int)((vbk + 1) * TK / G) - g0;
+  const TileWalk tw = xcd_tile_walk(T);
+  const int ntl = tw.count();
+  const int total = ntl * nk;                        // K-tiles this block computes
   if (total == 0) return;
-  auto tile_at = [&](int it) { return SK ? it : tw.at(it); };
+  auto tile_at = [&](int it) { return tw.at(it); };
 
   const auto xr = make_rsrc(p.x, p.xbytes);
   const auto wr = make_rsrc(p.w, p.wbytes);
@@ -1605,14 +1401,12 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
 
   // ---- staging cursors (A and B halves are staged in different phases, each in K-tile order)
-  int a_it = SK ? g0 / nk : 0, a_kt = SK ? g0 % nk : 0, b_it = a_it, b_kt = a_kt, a_gk = 0, b_gk = 0;
-  bool a_new = true, b_new = true;   // first staging: the block may start inside a tile (stream-K)
+  int a_it = 0, a_kt = 0, b_it = 0, b_kt = 0, a_gk = 0, b_gk = 0;
   uint32_t a_off[2][AP], b_off[2][BP], a_so = 0;
   KCursor<BKE> su;
   auto stage_a = [&](int h) {   // half h (0 / 1) of K-tile a_gk
     if (h == 0) {
-      if (a_kt == 0 || a_new) {
-        a_new = false;
+      if (a_kt == 0) {
         const int t = tile_at(a_it);
         PixelWalk pw(p, (t / nN) * BM + wave * 8 + lr);
 #pragma unroll
@@ -1633,10 +1427,8 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       if (++a_kt == nk) { a_kt = 0; ++a_it; }
     }
   };
-  constexpr int BFIRST = (OPT & 16) ? 0 : 1;   // which B half of a K-tile is staged first
-  auto stage_b = [&](int h) {   // half h of K-tile b_gk; staged B1 first, then B0 (OPT 16: B0, then B1)
-    if (h == BFIRST && (b_kt == 0 || b_new)) {
-      b_new = false;
+  auto stage_b = [&](int h) {   // half h of K-tile b_gk; staged B1 first, then B0
+    if (h == 1 && b_kt == 0) {
       const int n0 = tile_at(b_it) % nN * BN;
 #pragma unroll
       for (int q = 0; q < 2 * BP; ++q)
@@ -1646,7 +1438,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     unsigned char* d = smem + (b_gk & 1) * BUF + 2 * AHB + h * BHB;
 #pragma unroll
     for (int j = 0; j < BP; ++j) dma16(wr, d + (j * 8 + wave) * 8 * ROWB, b_off[h][j], (uint32_t)b_kt * BKE * 2);
-    if (h != BFIRST) {
+    if (h == 0) {
       ++b_gk;
       if (++b_kt == nk) { b_kt = 0; ++b_it; }
     }
@@ -1655,7 +1447,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   // ---- compute side
   f4 acc[2][2][2][4];
   int cm0 = 0, cn0 = 0;
-  auto init_tile = [&](int i, bool with_bias = true) {
+  auto init_tile = [&](int i) {
     const int t = tile_at(i);
     cm0 = (t / nN) * BM;
     cn0 = (t % nN) * BN;
@@ -1667,7 +1459,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
         f4 bv;
 #pragma unroll
         for (int e = 0; e < 4; ++e)
-          bv[e] = (with_bias && col + e < p.cout) ? (BIASB ? bias_l[col + e] : p.bias[col + e]) : 0.0f;
+          bv[e] = col + e < p.cout ? (BIASB ? bias_l[col + e] : p.bias[col + e]) : 0.0f;
 #pragma unroll
         for (int ha = 0; ha < 2; ++ha)
 #pragma unroll
@@ -1675,25 +1467,6 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       }
   };
   const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
-  // stream-K: the last arriver's epilogue sums the tile's segments (block order) fragment by fragment
-  struct SkSum { int nseg = 0, sown = 0, blo = 0; bool blo_first = false; };
-  SkSum sks;
-  const auto prs = make_rsrc(p.part, 0x7fffffffu);
-  auto seg_sum = [&](const f4& own, int q) -> f4 {
-    f4 v = own;
-    for (int s2 = 0; s2 < sks.nseg; ++s2) {
-      f4 x;
-      if (s2 == sks.sown) {
-        x = own;
-      } else {
-        const uint32_t sl = (uint32_t)((sks.blo + s2) * 2 + ((s2 == 0 && !sks.blo_first) ? 1 : 0));
-        x = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(prs, ((sl * 32 + q) * NTH + tid) * 16, 0,
-                                                                         CPOL_SC1));
-      }
-      v = s2 == 0 ? x : v + x;
-    }
-    return v;
-  };
   auto epilogue = [&]() {
 #pragma unroll
     for (int ha = 0; ha < 2; ++ha) {
@@ -1708,11 +1481,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
           typedef _Float16 h4 __attribute__((ext_vector_type(4)));
           typedef uint32_t u2 __attribute__((ext_vector_type(2)));
           h4 va, vb;
-          f4 a0 = acc[hb][0][ha][i], a1 = acc[hb][1][ha][i];
-          if (SK && sks.nseg > 1) {
-            a0 = seg_sum(a0, ((hb * 2 + 0) * 2 + ha) * 4 + i);
-            a1 = seg_sum(a1, ((hb * 2 + 1) * 2 + ha) * 4 + i);
-          }
+          const f4 a0 = acc[hb][0][ha][i], a1 = acc[hb][1][ha][i];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             va[e] = (_Float16)act_t<ACT>(a0[e]);
@@ -1730,56 +1499,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     }
   };
 
-  // stream-K hand-off of a tile cut between blocks (the split-K protocol of splitk_reduce: sc1 partial
-  // stores, every wave's vmcnt(0), a barrier, one lane's agent-scope atomic; the last arriver sums the
-  // segments in block order — the result does not depend on arrival order — and runs the epilogue).
-  // The two stagger groups are aligned around it (group 0 waits one barrier first, group 1 one after).
-  auto handoff = [&](int t, bool first) {
-    if (grp == 0) __builtin_amdgcn_s_barrier();
-    const uint32_t slot = (uint32_t)(vbk * 2 + (first ? 0 : 1));
-#pragma unroll
-    for (int q = 0; q < 32; ++q)
-      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, acc[q >> 4][(q >> 3) & 1][(q >> 2) & 1][q & 3]), prs,
-                                             ((slot * 32 + q) * NTH + tid) * 16, 0, CPOL_SC1);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const long tk0 = (long)t * nk;
-    const int blo = (int)(((tk0 + 1) * G - 1) / TK), bhi = (int)(((tk0 + nk) * G - 1) / TK);
-    const int nseg = bhi - blo + 1;
-    int* flag = reinterpret_cast<int*>(smem + 2 * BUF + BIASB);
-    if (tid == 0) {
-      const int old = __hip_atomic_fetch_add(p.cnt + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int last = old == nseg - 1;
-      if (last) __hip_atomic_store(p.cnt + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      *flag = last;
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    const bool last = *flag != 0;
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (last) {
-      sks.nseg = nseg;
-      sks.sown = vbk - blo;
-      sks.blo = blo;
-      sks.blo_first = (long)blo * TK / G == tk0;   // the tile is the first segment of block blo
-      epilogue();
-      sks.nseg = 0;
-    }
-    if (grp == 1) __builtin_amdgcn_s_barrier();
-  };
-
-  // ---- prologue: K-tile 0 whole, K-tile 1's A0, B1 and A1 in flight (OPT 16: all of K-tile 1)
-  if constexpr ((OPT & 16) != 0) {
-    static_assert((OPT & 16) == 0 || (BM == 256 && BN == 256), "OPT 16: 256 x 256 tiles only");
-    stage_a(0); stage_b(0); stage_b(1); stage_a(1);
-    if (total > 1) {
-      stage_a(0); stage_b(0); stage_b(1); stage_a(1);
-      asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-  } else {
+  // ---- prologue: K-tile 0 whole, K-tile 1's A0, B1 and A1 in flight
   stage_a(0); stage_b(1); stage_a(1); stage_b(0);
   if (total > 1) {
     stage_a(0); stage_b(1); stage_a(1);
@@ -1787,14 +1507,13 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
-  }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bias_l
   __builtin_amdgcn_s_barrier();
-  int ci = SK ? g0 / nk : 0, ckt = SK ? g0 % nk : 0, seg0 = ckt;   // compute cursor: tile, K step, segment start
-  init_tile(ci, ckt == 0);
+  int ci = 0, ckt = 0;   // compute cursor: tile, K step
+  init_tile(ci);
   if (grp == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind group 0
 
-  u4 xa[2][4], wb[2][2], wb1[2][2];   // wb1: OPT 16 keeps B half 1's fragments apart from half 0's
+  u4 xa[2][4], wb[2][2];
   auto read_a = [&](const unsigned char* h) {
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
@@ -1804,37 +1523,19 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
         xa[sb][i] = *reinterpret_cast<const u4*>(h + row * ROWB + swz(row, sb * 4 + g) * 16);
       }
   };
-  auto read_b_to = [&](const unsigned char* h, u4 (&w)[2][2]) {
+  auto read_b = [&](const unsigned char* h) {
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
         const int row = wn * 32 + j * 16 + li;
-        w[sb][j] = *reinterpret_cast<const u4*>(h + row * ROWB + swz(row, sb * 4 + g) * 16);
+        wb[sb][j] = *reinterpret_cast<const u4*>(h + row * ROWB + swz(row, sb * 4 + g) * 16);
       }
   };
-  auto read_b = [&](const unsigned char* h) { read_b_to(h, wb); };
-  auto mfma_qw = [&](int ha, int hb, const u4 (&w)[2][2]) {
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  auto mfma_q = [&](int ha, int hb) {
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this phase's reads retired (WAR: see above)
     __builtin_amdgcn_s_barrier();
     __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int sb = 0; sb < 2; ++sb)
-#pragma unroll
-      for (int j = 0; j < 2; ++j)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-          acc[hb][j][ha][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w[sb][j]),
-                                                                     __builtin_bit_cast(h8, xa[sb][i]),
-                                                                     acc[hb][j][ha][i], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
-  };
-  auto mfma_q = [&](int ha, int hb) {
-    if (!(OPT & 8) || grp == 1)
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this phase's reads retired (WAR: see above)
-    __builtin_amdgcn_s_barrier();
-    if (!(OPT & 2)) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
 #pragma unroll
@@ -1844,86 +1545,39 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
           acc[hb][j][ha][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[sb][j]),
                                                                      __builtin_bit_cast(h8, xa[sb][i]),
                                                                      acc[hb][j][ha][i], 0, 0, 0);
-    if (!(OPT & 2)) __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   };
 
-  if constexpr ((OPT & 16) != 0) {
-    // OPT 16: B half 0's fragments stay in registers from phase 0 to phase 3, so A0 and B0 are both
-    // free after phase 0: K-tile k+2 is staged whole in phases 1-3 (A0+B0, B1, A1) and the tile
-    // epilogue's stores, issued after phase 3, are younger than every load a later wait retires —
-    // phase 3 waits with vmcnt(8 [+ 16 while the previous tile's stores are in flight])
-    bool st = false;   // the epilogue after K-tile k-1 issued its stores
-    for (int k = 0; k < total; ++k) {
-      const unsigned char* bk = smem + (k & 1) * BUF;
-      const bool n2 = k + 2 < total;
-      read_b_to(bk + 2 * AHB, wb);
-      read_a(bk);
-      mfma_qw(0, 0, wb);
-      read_b_to(bk + 2 * AHB + BHB, wb1);
-      if (n2) { stage_a(0); stage_b(0); }
-      mfma_qw(0, 1, wb1);
-      read_a(bk + AHB);
-      if (n2) stage_b(1);
-      mfma_qw(1, 1, wb1);
-      if (n2) stage_a(1);
-      if (n2) {
-        if (st) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      } else {
-        if (st) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      st = false;
-      mfma_qw(1, 0, wb);
-      if (++ckt == nk) {
-        epilogue();
-        st = true;
-        ckt = 0;
-        if (++ci < ntl) init_tile(ci);
-      }
-    }
-    if (grp == 0) __builtin_amdgcn_s_barrier();
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    return;
-  }
   for (int k = 0; k < total; ++k) {
     const unsigned char* bk = smem + (k & 1) * BUF;
     const bool n1 = k + 1 < total, n2 = k + 2 < total;
-    constexpr bool DF = (OPT & 1) != 0;   // DMA first
     // phase 0: quadrant (0,0)
-    if (DF && n1) stage_b(0);
     read_b(bk + 2 * AHB);
     read_a(bk);
-    if (!DF && n1) stage_b(0);
+    if (n1) stage_b(0);
     mfma_q(0, 0);
     // phase 1: (0,1)
-    if (DF && n2) stage_a(0);
     read_b(bk + 2 * AHB + BHB);
-    if (!DF && n2) stage_a(0);
+    if (n2) stage_a(0);
     mfma_q(0, 1);
     // phase 2: (1,1)
-    if (DF && n2) stage_b(1);
     read_a(bk + AHB);
-    if (!DF && n2) stage_b(1);
+    if (n2) stage_b(1);
     mfma_q(1, 1);
     // phase 3: (1,0); K-tile k+1 retired (k+2's A0, B1 and A1 may stay in flight)
-    if (DF && n2) stage_a(1);
     read_b(bk + 2 * AHB);
     if (n2) {
-      if (!DF) stage_a(1);
+      stage_a(1);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     mfma_q(1, 0);
-    const bool tend = ++ckt == nk, rend = k == total - 1;
-    if (tend || (SK && rend)) {
-      if (!SK || (seg0 == 0 && tend)) epilogue();
-      else handoff(tile_at(ci), (long)tile_at(ci) * nk + seg0 == g0);
-      if (tend && !rend) {
+    if (++ckt == nk) {
+      epilogue();
+      if (k != total - 1) {
         ckt = 0;
-        seg0 = 0;
         init_tile(++ci);
       }
     }
@@ -1933,23 +1587,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
 }
 
 template <bool ONE>
-hipError_t launch_p8_sk(const ConvParams& p, int grid, hipStream_t st) {
-  if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 36>), dim3(grid), dim3(512), 0, st, p);
-  else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 2, 36>), dim3(grid), dim3(512), 0, st, p);
-  else YV7_LAUNCH((conv_f16_p8_kernel<ONE, 0, 36>), dim3(grid), dim3(512), 0, st, p);
-  return hipGetLastError();
-}
-
-template <bool ONE>
 hipError_t launch_p8_t(const ConvParams& p, int grid, hipStream_t st) {
-  if (p.act == 1 && p.variant == 233) {   // experiment: OPT 16 schedule (+ XCD order)
-    YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 20>), dim3(grid), dim3(512), 0, st, p);
-    return hipGetLastError();
-  }
-  // XCD-major tile order (OPT 4): 1x1 1024->1024 @40 140 -> 133 us, 3x3 layers unchanged (tune_ops)
-  if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1, 4>), dim3(grid), dim3(512), 0, st, p);
-  else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 2, 4>), dim3(grid), dim3(512), 0, st, p);
-  else YV7_LAUNCH((conv_f16_p8_kernel<ONE, 0, 4>), dim3(grid), dim3(512), 0, st, p);
+  if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 1>), dim3(grid), dim3(512), 0, st, p);
+  else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<ONE, 2>), dim3(grid), dim3(512), 0, st, p);
+  else YV7_LAUNCH((conv_f16_p8_kernel<ONE, 0>), dim3(grid), dim3(512), 0, st, p);
   return hipGetLastError();
 }
 
@@ -2188,8 +1829,6 @@ int env_variant() {
   return v;
 }
 
-constexpr size_t P8_PART = 256 * 256 * 4;   // one fp32 partial 256 x 256 tile (stream-K hand-off)
-
 // The dispatch's 8-phase-ring rule (launch_conv_f16 quotes the measurements behind it).
 bool p8_default(const ConvParams& p) {
   static const int on = [] { const char* e = getenv("YV7_P8"); return e ? atoi(e) : 1; }();
@@ -2201,54 +1840,12 @@ bool p8_default(const ConvParams& p) {
           (p.k == 3 && p.cin >= 256 && p.cin % BKE == 0));
 }
 
-// Stream-K form of the 8-phase ring (variant 237, or the dispatch with YV7_P8SK=1): the grid is every CU
-// and the layer's K-tiles are split evenly over it, so a layer with 200 tiles of 256 x 256 no longer
-// leaves 56 CUs idle; needs the split-K scratch (one partial tile per block and segment end).
-bool p8_streamk(const ConvParams& p) {
-  static const int sk = [] { const char* e = getenv("YV7_P8SK"); return e ? atoi(e) : 0; }();
-  const int variant = p.variant ? p.variant : env_variant();
-  return variant == 237 || (variant == 0 && sk && p8_default(p));
-}
-
 hipError_t launch_p8(const ConvParams& p, bool one, hipStream_t st) {
   if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || (!one && p.cin % BKE)) return hipErrorInvalidValue;
   const long T = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
   const int cus = device_cus();
-  if (p8_streamk(p) && p.part && p.cnt && p.part_bytes >= (size_t)cus * 2 * P8_PART && p.cnt_n >= T) {
-    // at most one block per K-tile: every block's range is non-empty, so the blocks between a tile's
-    // first and last are exactly its segments
-    const long TK = T * (p.kpad / BKE);
-    const int grid = (int)(TK < (long)cus ? TK : (long)cus);
-    return one ? launch_p8_sk<true>(p, grid, st) : launch_p8_sk<false>(p, grid, st);
-  }
   const int grid = (int)(T < (long)cus ? T : (long)cus);
   return one ? launch_p8_t<true>(p, grid, st) : launch_p8_t<false>(p, grid, st);
-}
-
-// the 8-phase ring on 512 x 128 tiles (128-channel layers)
-hipError_t launch_p8w(const ConvParams& p, bool one, hipStream_t st) {
-  if (p.cout > 128 || p.cout % 8 || p.yoff % 8 || p.yc % 8 || (!one && p.cin % BKE)) return hipErrorInvalidValue;
-  const long T = (long)((p.M + 511) / 512);
-  const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
-  if (one) {
-    if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<true, 1, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-    else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<true, 2, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-    else YV7_LAUNCH((conv_f16_p8_kernel<true, 0, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-  } else {
-    if (p.act == 1) YV7_LAUNCH((conv_f16_p8_kernel<false, 1, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-    else if (p.act == 2) YV7_LAUNCH((conv_f16_p8_kernel<false, 2, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-    else YV7_LAUNCH((conv_f16_p8_kernel<false, 0, 4, 512, 128>), dim3(grid), dim3(512), 0, st, p);
-  }
-  return hipGetLastError();
-}
-
-// 128-channel 3x3 stride-1 layers with at least one round of 512 x 128 tiles on the 8-phase ring
-// (variant 238) — YV7_P8W=1 (bench A/B under batches in flight: alone on the chip it ties the 2-phase
-// ring, the last partial round of its 400 tiles leaving CUs idle that other streams can fill).
-bool p8w_default(const ConvParams& p) {
-  static const int on = [] { const char* e = getenv("YV7_P8W"); return e ? atoi(e) : 0; }();
-  return on && !p.pool && p.k == 3 && p.s == 1 && p.cout == 128 && p.cin >= 128 && p.cin % BKE == 0 &&
-         p.yoff % 8 == 0 && p.yc % 8 == 0 && (long)((p.M + 511) / 512) >= device_cus();
 }
 
 hipError_t launch_p8n(const ConvParams& p, bool one, hipStream_t st) {
@@ -2256,21 +1853,6 @@ hipError_t launch_p8n(const ConvParams& p, bool one, hipStream_t st) {
   const long T = (long)((p.M + 255) / 256) * ((p.cout + 127) / 128);
   const int grid = (int)(T < (long)device_cus() ? T : (long)device_cus());
   return one ? launch_p8n_t<true>(p, grid, st) : launch_p8n_t<false>(p, grid, st);
-}
-
-template <int BM, int BN, int WM, int WN, bool ONE>
-hipError_t launch_pp(const ConvParams& p, int occ, hipStream_t st) {
-  if (p.cout > 1024 || p.cout % 8 || p.yoff % 8 || p.yc % 8) return hipErrorInvalidValue;
-  const long T = (long)((p.M + BM - 1) / BM) * ((p.cout + BN - 1) / BN);
-  const long cap = (long)device_cus() * occ;
-  const int grid = (int)(T < cap ? T : cap);
-  if (p.act == 1)
-    YV7_LAUNCH((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 1>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
-  else if (p.act == 2)
-    YV7_LAUNCH((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 2>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
-  else
-    YV7_LAUNCH((conv_f16_pp_kernel<BM, BN, WM, WN, ONE, 0>), dim3(grid), dim3(64 * WM * WN), 0, st, p);
-  return hipGetLastError();
 }
 
 // the N-split weight-stationary 1x1 ring (cout > BN: block b holds N tile (b / 8) % nN; three stages)
@@ -2424,14 +2006,12 @@ hipError_t launch_choice(const ConvParams& p, const Choice& c, bool one, hipStre
 }  // namespace
 
 size_t conv_splitk_part_bytes(const ConvParams& p) {
-  if (!p.pool && p8_streamk(p)) return (size_t)device_cus() * 2 * P8_PART;
   const Choice c = choose(p, false);   // (choose() keeps this under 2 GiB)
   if (c.cfg < 0 || c.S <= 1) return 0;
   return (size_t)ring_tiles(p, c.cfg) * c.S * cfg_bm[c.cfg] * cfg_bn[c.cfg] * 4;
 }
 
 int conv_splitk_tiles(const ConvParams& p) {
-  if (!p.pool && p8_streamk(p)) return (int)(((p.M + 255) / 256) * ((p.cout + 255) / 256));
   const Choice c = choose(p, false);
   return (c.cfg < 0 || c.S <= 1) ? 0 : (int)ring_tiles(p, c.cfg);
 }
@@ -2448,32 +2028,37 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (pcfg == 1) return launch_t<128, 128, 2, false, false, 1, true>(p, st);
     return launch_t<64, 128, 1, false, false, 1, true>(p, st);
   }
-  // the register-streamed 1x1 (conv_rs.hip; 240 forces it where it applies)
-  if (!det && variant == 240 && conv1x1_rs_supported(p, nullptr)) return launch_conv1x1_rs(p, nullptr, st);
-  // the 3x3 halo ring (conv_hring.hip): 260 = 128-channel tiles, 261 = 256-channel tiles
-  // (forced only where every N tile is full: the masked last tile of a cout that 128 does not divide has
-  // no layer in the checked networks — ADVICE r3)
-  if (!det && (variant == 260 || variant == 261 || variant == 262 || (variant >= 911 && variant <= 914)) &&
-      hring_supported(p) && p.cout % (variant == 261 ? 256 : 128) == 0)
-    return launch_conv_hring(p, variant == 261 ? 256 : variant == 260 ? 128 : 2, device_cus(), st);
+  // the column-group 3x3 halo ring (conv_hring.hip, variant 262; 911-914: its microbenchmark hooks),
+  // forced only where every N tile is full: the masked last tile of a cout that 128 does not divide has
+  // no layer in the checked networks
+  if (!det && (variant == 262 || (variant >= 911 && variant <= 914)) && hring_supported(p) && p.cout % 128 == 0)
+    return launch_conv_hring(p, device_cus(), st);
   // the low-resolution 3x3 kernel (conv_lr.hip): 270 + tile configuration
-  if (!det && variant >= 270 && variant <= 273 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
+  if (!det && variant >= 270 && variant <= 274 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
   // 3x3 stride-1 layers of up to 204 800 output pixels (yolov7 640 bs 32 from 80^2 down, yolov7-w6 1280
   // bs 8 from 160^2 down): the low-resolution kernel (conv_lr.hip) — one layer forced at a time in the bs-32
   // forward (profiles/r4lr/tune3.txt, us, dispatch -> lr): 3x3 256->256 @20 32.2 -> 22.1, 512->512 @20
   // 80.8 -> 62.7, 512->256 @20 48.8 -> 37.0, 512->1024 @20 119.8 -> 107.5, 128->128 @40 24.5 -> 21.9,
   // 256->128 @40 43.5 -> 35.6, 256->256 @40 69.9 -> 59.5, 256->512 @40 129.8 -> 108.5, 128->128 @80
   // 74.3 -> 63.4, 128->256 @80 123.9 -> 119.5, 128->64 @80 50.2 -> 40.8, 64->64 @80 31.6 -> 27.4.
-  // 80 x 128 tiles when there are >= 1000 of them, else 80 x 64 (64-pixel tiles when 5 does not divide
-  // the height).  YV7_LR=0: off.
+  // 80 x 128 tiles when there are >= 400 of them, else 80 x 64 (64-pixel tiles when 5 does not divide
+  // the height); w6 1280 bs 8 (profiles/r4lr/tune_w6.txt): 384->384 @40 38.7 -> 36.3 and 384->768 @40
+  // 73.0 -> 66.0 with 80 x 128 (480 / 960 tiles); yolov7's 512->512 @20 and 128->128 / 256->128 @40
+  // (640) are equal either way.  YV7_LR=0: off.
   static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
   if (!det && variant == 0 && lr && (long)p.M <= 204800 && p.k == 3 && p.s == 1 &&
       !((long)p.B * (p.H / 16) * (p.W / 16) >= 2048 && ws64_supported(p))) {
     const bool t5 = p.H % 5 == 0;
     const long t128 = (long)((p.B + 3) / 4) * (p.H / (t5 ? 5 : 4)) * (p.W / 4) * (p.cout / 128);
-    const int cfg = (p.cout % 128 == 0 && t128 >= 1000 ? 0 : 1) + (t5 ? 0 : 2);
+    const int cfg = (p.cout % 128 == 0 && t128 >= 400 ? 0 : 1) + (t5 ? 0 : 2);
     if (lr_supported(p, cfg)) return launch_conv_lr(p, cfg, st);
   }
+  // 3x3 stride-2 layers the 128 x 128 ring would split K for (under 256 of its tiles: yolov7's 256->256
+  // s2 @40, w6's 768->1024 s2 @40): the stride-2 low-resolution form (profiles/r4lr/convbench_s2.txt:
+  // 256->256 s2 @40 29.6 -> 25.4 us)
+  if (!det && variant == 0 && lr && p.k == 3 && p.s == 2 && (long)((p.M + 127) / 128) * ((p.cout + 127) / 128) <= 256 &&
+      lr_supported(p, 4))
+    return launch_conv_lr(p, 4, st);
   // 3x3 stride-1 layers with 128-channel output tiles and at least one round of 16 x 16 x 128 tiles: the
   // column-group halo ring (conv_hring.hip, variant 262).  Single-layer sweep, bs 32 640, same box
   // (profiles/r3_hring2_tune.txt, us, dispatch -> 262): 3x3 128->128 @80 80.0 / 80.4 / 82.7 / 81.0 ->
@@ -2481,7 +2066,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   static const int hring = [] { const char* e = getenv("YV7_HRING"); return e ? atoi(e) : 1; }();
   if (!det && variant == 0 && hring && hring_supported(p) && p.cout % 128 == 0 &&
       (long)p.B * (p.Ho / 16) * (p.Wo / 16) * (p.cout / 128) >= device_cus())
-    return launch_conv_hring(p, 2, device_cus(), st);
+    return launch_conv_hring(p, device_cus(), st);
   if (!det && variant == 0 && p.cout > 32 && p.cout <= 1024 && p.cout % 8 == 0) {
     // Persistent ring (scripts/convbench.hip, bs 32, same box, us): short-K 1x1 layers and the
     // 128-channel / low-resolution 512-channel 3x3 layers, whose per-tile fill + epilogue the
@@ -2531,8 +2116,6 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
         return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     } else if (wide && p.k == 3 && p.cin >= 256 && p.cout >= 256 && t256 >= 200) {
       return launch_pring<256, 256, 2, 4, 2>(p, one, 1, st);
-    } else if (p8w_default(p)) {
-      return launch_p8w(p, false, st);
     } else if (p.k == 3 && p.cout == 128) {
       // (3x3 512->512 @20 and s2 from @40 take the non-persistent 128 x 128 ring of choose() below:
       // in-network 92 (this ring) / 89 (256 x 128 persistent) -> 79 us; with fewer tiles than CUs,
@@ -2553,26 +2136,10 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 204) return launch_pring<128, 128, 2, 2, 2>(p, one, 2, st);
     if (variant == 205) return launch_pring<256, 128, 4, 2, 2>(p, one, 1, st);
     if (variant == 206) return launch_pring<128, 256, 2, 4, 2>(p, one, 1, st);
-    // BK 32 rings: twice the stages in the same LDS (more K steps in flight)
-    if (variant == 211) return launch_pring<256, 256, 2, 4, 4, 32>(p, one, 1, st);
-    if (variant == 212) return launch_pring<256, 128, 4, 2, 4, 32>(p, one, 1, st);
-    if (variant == 213) return launch_pring<128, 128, 2, 2, 4, 32>(p, one, 2, st);
-    if (variant == 214) return launch_pring<256, 256, 2, 4, 3, 32>(p, one, 1, st);
-    // 4-wave blocks, two per CU (blocks drift out of phase: one block's epilogue beside the other's MFMAs)
-    if (variant == 215) return launch_pring<256, 128, 2, 2, 3, 32>(p, one, 2, st);
-    if (variant == 216) return launch_pring<128, 256, 2, 2, 3, 32>(p, one, 2, st);
-    if (variant == 217) return launch_pring<128, 128, 2, 2, 2, 64>(p, one, 2, st);
-    // three blocks per CU (48 KiB of ring each): more waves to hide the ring's latency — measured
-    // 10-20 % slower than the dispatch on every 128-channel layer, bench 6626 vs 6801 img/s
-    // (profiles/r2c_pring3/): twice the barriers per K of 64 cost more than the extra waves hide
-    if (variant == 218) return launch_pring<128, 128, 2, 2, 3, 32>(p, one, 3, st);
-    // pipelined persistent rings (conv_f16_pp_kernel)
-    if (variant == 221) return one ? launch_pp<256, 256, 2, 4, true>(p, 1, st) : launch_pp<256, 256, 2, 4, false>(p, 1, st);
-    if (variant == 222) return one ? launch_pp<128, 128, 2, 2, true>(p, 2, st) : launch_pp<128, 128, 2, 2, false>(p, 2, st);
-    if (variant == 223) return one ? launch_pp<256, 128, 4, 2, true>(p, 1, st) : launch_pp<256, 128, 4, 2, false>(p, 1, st);
-    // 8-phase persistent ring (conv_f16_p8_kernel)
-    if ((variant == 231 || variant == 233 || variant == 237) && (one || p.cin % BKE == 0))
-      return launch_p8(p, one, st);
+    // 8-phase persistent ring (conv_f16_p8_kernel).  Round 4 removed the forced-only forms DESIGN §8
+    // records as slower (BK-32 and 3-per-CU rings 211-218, pipelined rings 221-223, the p8 schedules
+    // 233 / 237, the 512 x 128 p8 238, the first halo rings 260 / 261, the stand-alone 240).
+    if (variant == 231 && (one || p.cin % BKE == 0)) return launch_p8(p, one, st);
     // weight-stationary 1x1 rings (conv_f16_pring_kernel, WS): 234 = 128 x 256 tiles (K <= 256),
     // 235 = 256 x 128 (K <= 256), 236 = 128 x 128 (K <= 512)
     if (variant == 234 && one && p.cout <= 256 && p.kpad <= 256) return launch_pring_ws<128, 256, 2, 4, 4>(p, st);
@@ -2581,7 +2148,6 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // N-split weight-stationary 1x1 (K <= 256, 128 < cout <= 512): 256 x 128 tiles, three stages
     if (variant == 239 && one && p.cout > 128 && p.cout <= 512 && p.kpad <= 256) return launch_pring_wsn<256, 128, 4, 2, 4>(p, st);
     if (variant == 232 && (one || p.cin % BKE == 0)) return launch_p8n(p, one, st);
-    if (variant == 238 && p.cout <= 128 && (one || p.cin % BKE == 0)) return launch_p8w(p, one, st);
   }
   if (!det && p.cout > 32) {
     // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/

@@ -1,30 +1,17 @@
-// 3x3 / stride-1 / pad-1 fp16 convolution as a persistent "halo ring" on gfx950 — the 128- and
-// 256-channel 3x3 layers of the ELAN stacks at 80x80 and above (cfg/deploy/yolov7.yaml: 128->128 x4
-// and the 128->256 RepConv at 80; yolov7-w6's wide stages at 160 / 320).  Replaces, like
+// 3x3 / stride-1 / pad-1 fp16 convolution as a persistent "halo ring" on gfx950 (variant 262) — the
+// 128-channel-output 3x3 layers with at least one round of 16 x 16 output tiles.  Replaces, like
 // conv_f16.hip, Conv.fuseforward (models/common.py:110-111) and RepConv's deploy conv
-// (common.py:498-500): y = act(conv2d(x, W', b', s=1, pad=1)).
+// (common.py:498-500): y = act(conv2d(x, W', b', s=1, pad=1)).  Round 3 made it the default for the
+// 128-channel layers at 80^2; round 4's conv_lr.hip (weights straight to VGPRs, 4-image x 4-column pixel
+// fragments) took those layers over (profiles/r4lr/tune3.txt: 3x3 128->128 @80 74.3 -> 63.4 us), so the
+// default dispatch picks this kernel only for 128-multiple-channel layers of more than 204 800 output
+// pixels.
 //
 // Why: the implicit-GEMM rings stage one tap's A tile per K step, so every input pixel crosses the
-// L2 -> LDS path nine times and a 128 x 128 tile moves 1/128 byte per FLOP — on these layers the
-// kernels run at 25-30 % MFMA busy whatever their schedule (profiles/r2_pmc_families.txt,
-// r2_tune_ops.txt).  Here:
-//  * a block owns a 16 x 16 output tile of one image x BN output channels; per 32-channel chunk the
-//    18 x 18 input patch (zero frame included, yv7_kernels.h BORDER) is DMA'd into LDS ONCE and all
-//    nine taps read their pixel fragments from it — tap (r, s) of output pixel (y, x) is patch pixel
-//    (y + r) * 18 + x + s — so the activation bytes per FLOP fall ~7x and weights dominate the
-//    (3x smaller) L2 -> LDS stream;
-//  * one phase = one (chunk, tap) K step of 32: the BN x 32 weight stage streams through an R-deep
-//    LDS-DMA ring (buffer_load ... lds, lane-linear, swizzle applied on the source address), the
-//    next chunk's patch into the other of two patch buffers during the first three phases of a chunk;
-//  * 8 waves = 4 (output rows) x 2 (channel halves), two per SIMD in two stagger groups offset by
-//    one barrier (cdna_hip_programming.md §5 8-phase template): a phase is {fragment reads, DMA
-//    issue, counted vmcnt, lgkmcnt(0), barrier, 16 x (BN / 128) MFMAs 16x16x32, barrier}, so one
-//    group's MFMA cluster runs beside the other group's LDS reads and DMA issue;
-//  * every wave issues the same DMA sequence (dummies past the block's last tile), so every wait is a
-//    compile-time vmcnt; tile epilogue stores in flight add a known count for the R - 2 phases after;
-//  * persistent XCD-major tile walk (TileWalk), epilogue straight from the accumulators (bias in the
-//    accumulators, compile-time activation, fp16, permlane16 pairing, 16-byte NHWC stores into the
-//    output channel slice: zero-copy concat).
+// L2 -> LDS path nine times.  Here a block owns a 16 x 16 output tile of one image x 128 output
+// channels; per 32-channel chunk the 18 x 18 input patch (zero frame included, yv7_kernels.h BORDER)
+// is DMA'd into LDS ONCE and all nine taps read their pixel fragments from it — tap (r, s) of output
+// pixel (y, x) is patch pixel (y + r) * 18 + x + s.  The schedule is described at the kernel.
 // LDS rows are 64 bytes (32 fp16); the 16-byte chunk c of row q sits in slot c ^ ((q >> 1) & 3)
 // (patch: q's column px instead of q) — conflict-free ds_read_b128 for every tap offset (checked
 // exhaustively against the gfx950 lane groups, MI355X_MICROARCH.md §LDS).
@@ -41,30 +28,12 @@ constexpr int PS = TS + 2;             // patch side
 constexpr int PPIX = PS * PS;          // 324 patch pixels
 constexpr int CK = 32;                 // channels per phase (one MFMA K step)
 constexpr int ROWB = CK * 2;           // 64 bytes per LDS row
-constexpr int PPW = 3;                 // patch DMA pieces per wave per chunk (24 pieces = 384 rows >= 324)
-constexpr int PBUF = 8 * PPW * 1024;   // one patch buffer
+constexpr int PPW = 3;                 // patch DMA pieces per wave per chunk (24 pieces: 21 rows of 16 pixels + 3 dummies)
 constexpr int NTH = 512;
 constexpr uint32_t OOB = 0x80000000u;  // a buffer offset past every tensor: DMA writes zeros
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t vo, uint32_t so) {
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, vo, so, 0, 0);
-}
-
-// vmcnt of phase i's wait (phase-in-chunk i = 0..8): the DMA ops a wave has issued after the weight
-// stage the next phase reads (issued R - 2 phases earlier, then one stage of PWN pieces per phase and
-// one patch piece in phases 0..PPW-1 of every chunk, patch after weights); in phase 8 also the next
-// chunk's patch, whose last piece was issued in phase PPW - 1.
-constexpr int wait_count(int i, int R, int PWN) {
-  int n = (R - 2) * PWN;
-  for (int k = 0; k <= R - 2; ++k) {
-    const int ii = ((i - k) % 9 + 9) % 9;
-    if (ii < PPW) ++n;
-  }
-  if (i == 8) {
-    const int np = (8 - (PPW - 1)) * PWN;
-    if (np < n) n = np;
-  }
-  return n;
 }
 
 // The counted waits assume each wave's vector-memory ops issue exactly as written: every dummy DMA
@@ -81,240 +50,9 @@ __device__ __forceinline__ void vmwait() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int BN, int R, int ACT>
-__global__ __launch_bounds__(NTH, 1) void conv3x3_hring_kernel(const ConvParams p) {
-  constexpr int WNC = BN / 2;               // output channels per wave
-  constexpr int TN = WNC / 16;              // n-fragments per wave
-  constexpr int TM = 4;                     // m-fragments per wave: 4 output rows of 16 pixels
-  constexpr int STG = BN * ROWB;            // one weight stage: BN rows x 32 k
-  constexpr int PWN = BN / 128;             // weight pieces per wave per stage
-  constexpr int NST = TM * TN / 2;          // epilogue stores per lane per tile
-  constexpr int RING = 2 * PBUF;
-  constexpr int BIAS = RING + R * STG;
-  constexpr int DUMMY = BIAS + 4096;         // PWN + 1 KiB: one distinct slot per dummy of a phase
-  constexpr int LDS = DUMMY + (PWN + 1) * 1024;
-  static_assert(LDS <= 160 * 1024, "LDS budget");
-  static_assert(TN % 2 == 0 && PWN >= 1, "tile shape");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
-  float* bias_l = reinterpret_cast<float*>(smem + BIAS);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-  const int grp = wave >> 2;                // stagger group: one wave of each per SIMD
-  const int g = lane >> 4, li = lane & 15;
-
-  const int nN = (p.cout + BN - 1) / BN;
-  const int txn = p.Wo / TS, tyn = p.Ho / TS;
-  const int T = p.B * tyn * txn * nN;
-  const int nch = p.cin / CK;
-  const TileWalk tw = xcd_tile_walk(T);
-  const int ntl = tw.count();
-  if (ntl == 0) return;
-
-  const auto xr = make_rsrc(p.x, p.xbytes);
-  const auto wr = make_rsrc(p.w, p.wbytes);
-  const auto yr = make_rsrc(p.y, 0x7fffffffu);
-  for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
-
-  struct Tile { int b, y0, x0, n0; };
-  auto tile = [&](int it) {
-    int t = tw.at(it);
-    Tile d;
-    d.n0 = (t % nN) * BN;
-    t /= nN;
-    d.x0 = (t % txn) * TS;
-    t /= txn;
-    d.y0 = (t % tyn) * TS;
-    d.b = t / tyn;
-    return d;
-  };
-
-  // ---- weight-stage issue cursor (stage = (tile, chunk, tap), tile-major), PWN pieces per wave
-  int w_it = 0, w_c = 0, w_t = 0, w_slot = 0;
-  uint32_t wvo[PWN];
-  const int wlr = lane >> 2;                                  // row within a 16-row piece
-  const int wsrc = (lane & 3) ^ ((lane >> 3) & 3);            // source chunk of this lane's slot
-  auto w_offsets = [&](int n0) {
-#pragma unroll
-    for (int j = 0; j < PWN; ++j)
-      wvo[j] = (uint32_t)(((n0 + (wave + 8 * j) * 16 + wlr) * p.kpad + wsrc * 8) * 2);
-  };
-  w_offsets(tile(0).n0);
-  auto issue_w = [&]() __attribute__((always_inline)) {
-    unsigned char* d = smem + RING + w_slot * STG;
-    if (w_it < ntl) {
-      const uint32_t so = (uint32_t)((w_t * p.cin + w_c * CK) * 2);
-#pragma unroll
-      for (int j = 0; j < PWN; ++j) dma16(wr, d + (wave + 8 * j) * 1024, wvo[j], so);
-    } else {   // past the block's last tile: same op count, nothing fetched
-#pragma unroll
-      for (int j = 0; j < PWN; ++j) dma16(wr, smem + DUMMY + j * 1024, OOB, 0u);
-    }
-    dma_fence();
-    if (++w_slot == R) w_slot = 0;
-    if (++w_t == 9) {
-      w_t = 0;
-      if (++w_c == nch) {
-        w_c = 0;
-        if (++w_it < ntl && nN > 1) w_offsets(tile(w_it).n0);
-      }
-    }
-  };
-
-  // ---- patch issue cursor: chunk (p_it, p_c) into buffer p_gc & 1, piece wave + 8 j of 24
-  int p_it = 0, p_c = 0, p_gc = 0;
-  uint32_t pvo[PPW];
-  auto p_offsets = [&](int it) {
-    const Tile d = tile(it);
-#pragma unroll
-    for (int j = 0; j < PPW; ++j) {
-      const int pp = (wave + 8 * j) * 16 + (lane >> 2);
-      const int py = pp / PS, px = pp - py * PS;
-      const int src = (lane & 3) ^ ((px >> 1) & 3);
-      pvo[j] = pp < PPIX ? (uint32_t)((pix_index(d.b, d.y0 - 1 + py, d.x0 - 1 + px, p.H, p.W) * p.xc + p.xoff + src * 8) * 2)
-                         : OOB;
-    }
-  };
-  p_offsets(0);
-  auto issue_p = [&](int j) __attribute__((always_inline)) {
-    if (p_it < ntl) dma16(xr, smem + (p_gc & 1) * PBUF + (wave + 8 * j) * 1024, pvo[j], (uint32_t)p_c * CK * 2);
-    else dma16(xr, smem + DUMMY + PWN * 1024, OOB, 0u);
-    dma_fence();
-    if (j == PPW - 1) {
-      ++p_gc;
-      if (++p_c == nch) {
-        p_c = 0;
-        if (++p_it < ntl) p_offsets(p_it);
-      }
-    }
-  };
-
-  // ---- compute side
-  f4 acc[TN][TM];
-  int c_it = 0, c_c = 0, c_gc = 0, c_slot = 0;
-  Tile ct = tile(0);
-  auto init_tile = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j) {
-      const int col = ct.n0 + wn * WNC + j * 16 + g * 4;
-      f4 bv;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? bias_l[col + e] : 0.0f;
-#pragma unroll
-      for (int ii = 0; ii < TM; ++ii) acc[j][ii] = bv;
-    }
-  };
-  const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
-  auto epilogue = [&]() __attribute__((always_inline)) {
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int ii = 0; ii < TM; ++ii) asm volatile("" : "+v"(acc[j][ii]));
-#pragma unroll
-    for (int ii = 0; ii < TM; ++ii) {
-      const int y = ct.y0 + wm * TM + ii, x = ct.x0 + li;
-      const uint32_t yo = (uint32_t)((pix_index(ct.b, y, x, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
-#pragma unroll
-      for (int mp = 0; mp < TN / 2; ++mp) {
-        typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-        typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-        h4 va, vb;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          va[e] = (_Float16)act_t<ACT>(acc[2 * mp][ii][e]);
-          vb[e] = (_Float16)act_t<ACT>(acc[2 * mp + 1][ii][e]);
-        }
-        const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
-        const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
-        const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
-        const u4 v = {s0[0], s1[0], s0[1], s1[1]};
-        const int n = ct.n0 + wn * WNC + mp * 32 + (int)lane_ch;
-        const uint32_t off = n < p.cout ? yo + (uint32_t)n * 2 : 0xffffffffu;
-        __builtin_amdgcn_raw_buffer_store_b128(v, yr, off, 0, 0);
-      }
-    }
-  };
-
-  // per-lane fragment read offsets: pixel fragments (patch pixel li + s of the wave's rows, slot
-  // g ^ key(column)) and weight fragments (stage row wn * WNC + j * 16 + li)
-  uint32_t a_lane[3];
-#pragma unroll
-  for (int s = 0; s < 3; ++s) a_lane[s] = (uint32_t)((li + s) * ROWB + ((g ^ (((li + s) >> 1) & 3)) * 16));
-  const uint32_t b_lane = (uint32_t)(li * ROWB + ((g ^ ((li >> 1) & 3)) * 16) + wn * WNC * ROWB);
-  const uint32_t a_wave = (uint32_t)(wm * TM * PS * ROWB);
-
-  // ---- prologue: chunk 0's patch, then weight stages 0 .. R-2
-#pragma unroll
-  for (int j = 0; j < PPW; ++j) issue_p(j);
-  for (int s0 = 0; s0 < R - 1; ++s0) issue_w();
-  vmwait<(R - 2) * PWN>();                      // patch 0 and stage 0 landed
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // bias_l
-  __builtin_amdgcn_s_barrier();
-  init_tile();
-  if (grp == 1) __builtin_amdgcn_s_barrier();   // group 1 runs one barrier behind group 0
-
-  int st_left = 0;   // phases whose wait must also count this wave's epilogue stores
-  auto phase = [&](auto ic) __attribute__((always_inline)) {
-    constexpr int i = decltype(ic)::value;
-    constexpr int r = i / 3, s = i % 3;
-    const unsigned char* pb = smem + (c_gc & 1) * PBUF + a_wave;
-    const unsigned char* wb_ = smem + RING + c_slot * STG;
-    u4 xa[TM], wb[TN];
-#pragma unroll
-    for (int ii = 0; ii < TM; ++ii)
-      xa[ii] = *reinterpret_cast<const u4*>(pb + a_lane[s] + ((ii + r) * PS) * ROWB);
-#pragma unroll
-    for (int j = 0; j < TN; ++j) wb[j] = *reinterpret_cast<const u4*>(wb_ + b_lane + j * 16 * ROWB);
-    issue_w();
-    if constexpr (i < PPW) issue_p(i);
-    constexpr int N = wait_count(i, R, PWN);
-    if (st_left > 0) {
-      vmwait<N + NST>();
-      --st_left;
-    } else {
-      vmwait<N>();
-    }
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // this phase's reads retired (WAR on the ring)
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int j = 0; j < TN; ++j)
-#pragma unroll
-      for (int ii = 0; ii < TM; ++ii)
-        acc[j][ii] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]), __builtin_bit_cast(h8, xa[ii]),
-                                                           acc[j][ii], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
-    if (++c_slot == R) c_slot = 0;
-  };
-
-  for (;;) {
-    phase(std::integral_constant<int, 0>{});
-    phase(std::integral_constant<int, 1>{});
-    phase(std::integral_constant<int, 2>{});
-    phase(std::integral_constant<int, 3>{});
-    phase(std::integral_constant<int, 4>{});
-    phase(std::integral_constant<int, 5>{});
-    phase(std::integral_constant<int, 6>{});
-    phase(std::integral_constant<int, 7>{});
-    phase(std::integral_constant<int, 8>{});
-    ++c_gc;
-    if (++c_c == nch) {
-      epilogue();
-      st_left = R - 2;
-      c_c = 0;
-      if (++c_it == ntl) break;
-      ct = tile(c_it);
-      init_tile();
-    }
-  }
-  if (grp == 0) __builtin_amdgcn_s_barrier();   // equal barrier counts in both groups
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-}
-
 // ---------------------------------------------------------------------------------------------
-// Halo ring, column-group form (variant 262).  Measured on the form above (PMC, 3x3 128->128 @80,
+// Halo ring, column-group form (variant 262).  Measured on round 3's first form (one tap per phase,
+// removed in round 4; PMC, 3x3 128->128 @80,
 // profiles/r3_pmc_128.txt): 32 % MFMA busy, 37 % of wave time parked at barriers / waits — a phase of
 // 16 MFMAs (256 cycles per wave) is shorter than the other group's read segment (8 fragment reads +
 // their LDS latency + a DMA issue + the counted wait), so the read segments, not the MFMAs, pace the
@@ -626,16 +364,6 @@ __global__ __launch_bounds__(NTH, 1) void conv3x3_hring2_kernel(const ConvParams
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
-template <int BN, int R>
-hipError_t launch_bn(const ConvParams& p, int cus, hipStream_t st) {
-  const long T = (long)p.B * (p.Ho / TS) * (p.Wo / TS) * ((p.cout + BN - 1) / BN);
-  const int grid = (int)(T < cus ? T : cus);
-  if (p.act == 1) YV7_LAUNCH((conv3x3_hring_kernel<BN, R, 1>), dim3(grid), dim3(NTH), 0, st, p);
-  else if (p.act == 2) YV7_LAUNCH((conv3x3_hring_kernel<BN, R, 2>), dim3(grid), dim3(NTH), 0, st, p);
-  else YV7_LAUNCH((conv3x3_hring_kernel<BN, R, 0>), dim3(grid), dim3(NTH), 0, st, p);
-  return hipGetLastError();
-}
-
 }  // namespace
 
 bool hring_supported(const ConvParams& p) {
@@ -644,29 +372,25 @@ bool hring_supported(const ConvParams& p) {
          p.Ho == p.H && p.Wo == p.W && p.Ho % TS == 0 && p.Wo % TS == 0;
 }
 
-// bn: 128 (variant 260) or 256 (variant 261); form 2: the column-group halo ring (variant 262)
-hipError_t launch_conv_hring(const ConvParams& p, int bn, int cus, hipStream_t st) {
+// the column-group halo ring (variant 262)
+hipError_t launch_conv_hring(const ConvParams& p, int cus, hipStream_t st) {
   if (!hring_supported(p)) return hipErrorInvalidValue;
-  if (bn == 2) {
-    // balanced persistent grid: every block the same number of tiles (the rest of the CUs stay free
-    // for other streams' kernels rather than running a short last round)
-    const long T = (long)p.B * (p.Ho / TS) * (p.Wo / TS) * ((p.cout + 127) / 128);
-    const long per = (T + cus - 1) / cus;
-    const int grid = (int)((T + per - 1) / per);
-    if (p.act == 1 && p.variant >= 911 && p.variant <= 914) {   // microbenchmark hooks (convbench only)
-      if (p.variant == 911) YV7_LAUNCH((conv3x3_hring2_kernel<1, 1>), dim3(grid), dim3(NTH), 0, st, p);
-      else if (p.variant == 912) YV7_LAUNCH((conv3x3_hring2_kernel<1, 2>), dim3(grid), dim3(NTH), 0, st, p);
-      else if (p.variant == 913) YV7_LAUNCH((conv3x3_hring2_kernel<1, 3>), dim3(grid), dim3(NTH), 0, st, p);
-      else YV7_LAUNCH((conv3x3_hring2_kernel<1, 4>), dim3(grid), dim3(NTH), 0, st, p);
-      return hipGetLastError();
-    }
-    if (p.act == 1) YV7_LAUNCH((conv3x3_hring2_kernel<1>), dim3(grid), dim3(NTH), 0, st, p);
-    else if (p.act == 2) YV7_LAUNCH((conv3x3_hring2_kernel<2>), dim3(grid), dim3(NTH), 0, st, p);
-    else YV7_LAUNCH((conv3x3_hring2_kernel<0>), dim3(grid), dim3(NTH), 0, st, p);
+  // balanced persistent grid: every block the same number of tiles (the rest of the CUs stay free for
+  // other streams' kernels rather than running a short last round)
+  const long T = (long)p.B * (p.Ho / TS) * (p.Wo / TS) * ((p.cout + 127) / 128);
+  const long per = (T + cus - 1) / cus;
+  const int grid = (int)((T + per - 1) / per);
+  if (p.act == 1 && p.variant >= 911 && p.variant <= 914) {   // microbenchmark hooks (convbench only)
+    if (p.variant == 911) YV7_LAUNCH((conv3x3_hring2_kernel<1, 1>), dim3(grid), dim3(NTH), 0, st, p);
+    else if (p.variant == 912) YV7_LAUNCH((conv3x3_hring2_kernel<1, 2>), dim3(grid), dim3(NTH), 0, st, p);
+    else if (p.variant == 913) YV7_LAUNCH((conv3x3_hring2_kernel<1, 3>), dim3(grid), dim3(NTH), 0, st, p);
+    else YV7_LAUNCH((conv3x3_hring2_kernel<1, 4>), dim3(grid), dim3(NTH), 0, st, p);
     return hipGetLastError();
   }
-  if (bn == 256) return launch_bn<256, 6>(p, cus, st);
-  return launch_bn<128, 8>(p, cus, st);
+  if (p.act == 1) YV7_LAUNCH((conv3x3_hring2_kernel<1>), dim3(grid), dim3(NTH), 0, st, p);
+  else if (p.act == 2) YV7_LAUNCH((conv3x3_hring2_kernel<2>), dim3(grid), dim3(NTH), 0, st, p);
+  else YV7_LAUNCH((conv3x3_hring2_kernel<0>), dim3(grid), dim3(NTH), 0, st, p);
+  return hipGetLastError();
 }
 
 }  // namespace yv7

@@ -269,12 +269,13 @@ hipError_t launch_nch(const ConvParams& p, hipStream_t st) {
 // configurations (profiles/r4lr/tune{1,2,3}.txt, one layer forced at a time in the yolov7 bs-32
 // forward): 4-wave blocks of 80-pixel tiles with the weights three column steps ahead won every layer
 // shape; the 8-wave and 128 / 160-pixel tiles, and two steps of prefetch, lost by 5-20 %.  0: 80 x 128,
-// 1: 80 x 64; 2 / 3: the same with 64-pixel tiles for heights that 5 does not divide.  The same four at
-// stride 2 were correct but slower than the dispatch on five of the six yolov7 stride-2 layers
-// (profiles/r4lr/convbench_s2.txt: 64->128 s2 @320 243 vs 215 us, 256->256 s2 @80 77 vs 68; a 9-column,
-// 2*TH+1-row patch per 80 outputs is 4.9 input pixels per output against 2.1 at stride 1), so none is
-// instantiated; the kernel keeps S as a parameter.
-#define LR_CFGS(X) X(0, 1, 4, 2, 5, 3, 1) X(1, 1, 4, 1, 5, 3, 1) X(2, 1, 4, 2, 4, 3, 1) X(3, 1, 4, 1, 4, 3, 1)
+// 1: 80 x 64; 2 / 3: the same with 64-pixel tiles for heights that 5 does not divide.  4: stride 2,
+// 64 x 128.  At stride 2 the same four were correct but slower than the dispatch on the large yolov7
+// stride-2 layers (profiles/r4lr/convbench_s2.txt: 64->128 s2 @320 243 vs 215 us, 256->256 s2 @80 77
+// vs 68: a 9-column, 2*TH+1-row patch per output tile is 4-5 input pixels per output against 2.1 at
+// stride 1) and faster only where the dispatch split K: 256->256 s2 @40 25.4 vs 29.6.
+#define LR_CFGS(X) \
+  X(0, 1, 4, 2, 5, 3, 1) X(1, 1, 4, 1, 5, 3, 1) X(2, 1, 4, 2, 4, 3, 1) X(3, 1, 4, 1, 4, 3, 1) X(4, 1, 4, 2, 4, 3, 2)
 #define LR_ROW(i, wm, wn, tn, tm, pd, s) {wm, wn, tn, tm, pd, s},
 constexpr int LR_CFG[][6] = {LR_CFGS(LR_ROW)};
 constexpr int LR_NCFG = sizeof(LR_CFG) / sizeof(LR_CFG[0]);

@@ -113,9 +113,9 @@ int kpad_of(const yv7_op_desc& o) {
   return (o.k * o.k * o.cin + 63) / 64 * 64;
 }
 bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7_WFMT_FP8; }
-// 3x3 / stride-1 / pad-1 fp16 convs get a fragment-packed weight copy (conv_lr.hip)
+// 3x3 / stride-1 or 2 / pad-1 fp16 convs get a fragment-packed weight copy (conv_lr.hip)
 bool wants_frag(int dtype, const yv7_op_desc& o) {
-  return dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && o.k == 3 && o.s == 1 && o.pad == 1 && !o.pool &&
+  return dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && o.k == 3 && (o.s == 1 || o.s == 2) && o.pad == 1 && !o.pool &&
          o.cin % 32 == 0;
 }
 
@@ -398,8 +398,8 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (kind == YV7_OP_DETECT) return v == 92 || v == 97 || v == 99;
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
-  return (v >= 201 && v <= 206) || (v >= 211 && v <= 218) || (v >= 221 && v <= 223) || (v >= 231 && v <= 240) ||
-         (v >= 260 && v <= 262) || (v >= 270 && v <= 273);
+  return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
+         (v >= 270 && v <= 274);
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {

@@ -212,7 +212,7 @@ bool lr_supported(const ConvParams& p, int cfg);
 hipError_t launch_conv_lr(const ConvParams& p, int cfg, hipStream_t st);
 size_t frag3x3_bytes(int cin, int cout);
 hipError_t pack_frag3x3(const void* w, int kpad, int cin, int cout, void* out, hipStream_t st);
-hipError_t launch_conv_hring(const ConvParams& p, int bn, int cus, hipStream_t st);
+hipError_t launch_conv_hring(const ConvParams& p, int cus, hipStream_t st);
 hipError_t launch_input(int dtype, const void* x, int x_dtype, void* y, int B, int H, int W, int yc,
                         bool reorg, hipStream_t st);
 hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int Ho,

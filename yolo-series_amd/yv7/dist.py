@@ -6,6 +6,8 @@ north star names:
   * broadcast_weights: rank 0 packs the fused network once; the packed blob (73.9 MB fp16 for
     yolov7) goes to every rank with one RCCL broadcast over xGMI, so every rank runs bit-identical
     weights without re-folding them.
+  * broadcast_fp8_plan (BASELINE configs[4]): rank 0 calibrates the fp8 activation scales, every rank
+    receives them (one small broadcast) before the weight blob, so every rank quantizes identically.
   * gather_detections: the fixed-shape per-rank NMS outputs (det [b,300,6] fp32, src_row [b,300]
     int64, count [b] int32) are all-gathered once per batch (~0.3 MB per rank for b = 32) so every
     rank holds the detections of the whole global batch in global image order.
@@ -46,16 +48,51 @@ def broadcast_weights(model, device, dtype, group=None):
     return Plan(g, device, broadcast_blob(g, device, group))
 
 
-def gather_detections(det, src_row, count, group=None, force=False):
+def broadcast_fp8_scales(scales, ops, device, group=None):
+    """Rank 0's {op: activation scale} for the fp8 ops `ops` (the same list on every rank: it comes from
+    the host-side graph) -> the same dict on every rank, by one broadcast."""
+    if dist.get_rank(group) == 0:
+        t = torch.tensor([float(scales[i]) for i in ops], dtype=torch.float64, device=device)
+    else:
+        t = torch.zeros(len(ops), dtype=torch.float64, device=device)
+    if len(ops):
+        dist.broadcast(t, src=0, group=group)
+    return {i: float(v) for i, v in zip(ops, t.tolist())}
+
+
+def broadcast_fp8_plan(model, device, min_cout=None, calib=None, group=None, scales=None):
+    """BASELINE configs[4] on N ranks: rank 0 calibrates (Plan.fp8_scales) — or takes `scales` — every
+    rank receives the scales, compiles the fp8 graph with them, and gets rank 0's packed blob, as
+    broadcast_weights does for the fp16 plan.  Returns (plan, graph); plan is None on a CPU device (the
+    --plumbing check)."""
+    from yv7.graph import FP8_MIN_COUT, fp8_candidates
+    min_cout = FP8_MIN_COUT if min_cout is None else min_cout
+    ops = fp8_candidates(compile_model(model, L.DT_F16), min_cout)
+    if dist.get_rank(group) == 0 and scales is None:
+        scales = Plan.fp8_scales(model, device, calib, min_cout)
+    scales = broadcast_fp8_scales(scales, ops, device, group)
+    g = compile_model(model, L.DT_F16, fp8=scales)
+    blob = broadcast_blob(g, device, group)
+    return (None if torch.device(device).type == 'cpu' else Plan(g, device, blob)), g, blob
+
+
+def gather_detections(det, src_row, count, group=None, force=False, sizes=None):
     """All-gather fixed-shape per-rank NMS outputs -> global (det, src_row, count) in image order.
     One rank: the inputs themselves, unless force (the collective is then issued anyway — a one-GPU
-    check of the RCCL path)."""
+    check of the RCCL path).  sizes: every rank's image count (shard()), when they differ: each rank's
+    rows are padded to the largest and the padding is dropped after the gather."""
     world = dist.get_world_size(group)
     if world == 1 and not force:
         return det, src_row, count
+    b = det.shape[0]
+    mx = max(sizes) if sizes else b
     outs = []
     for t in (det, src_row, count):
-        o = torch.empty((world * t.shape[0],) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        if mx != b:
+            t = torch.cat([t, torch.zeros((mx - b,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)])
+        o = torch.empty((world * mx,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(o, t.contiguous(), group=group)
+        if sizes and any(n != mx for n in sizes):
+            o = torch.cat([o[r * mx:r * mx + n] for r, n in enumerate(sizes)])
         outs.append(o)
     return tuple(outs)

@@ -127,12 +127,18 @@ class Plan:
     def fp8_from_model(cls, model, device, calib=None, min_cout=None):
         """BASELINE configs[4]: the fp16 plan with every 1x1 stride-1 conv (the Detect head excepted) on
         OCP e4m3 weights (per-output-channel scales) and e4m3 activations (per-tensor power-of-two
-        scales), through the block-scaled fp8 MFMA (csrc/conv_f8.hip).
+        scales), through the block-scaled fp8 MFMA (csrc/conv_f8.hip); scales from fp8_scales.
+        (Multi-GPU: yv7.dist.broadcast_fp8_plan calibrates on rank 0 and broadcasts.)"""
+        g = compile_model(model, L.DT_F16, fp8=cls.fp8_scales(model, device, calib, min_cout))
+        return cls(g, device, g.weight_blob().to(device))
 
-        Activation scales come from calibration: the fp16 plan runs `calib` ([B,3,H,W] frames in [0,1];
-        default: 2 seeded synthetic frames at the model's native size) and each fp8 op's input amax
-        sets xscale = 2**ceil(log2(amax / 448)), so the largest calibrated value still fits e4m3.
-        min_cout: which eligible 1x1 convs go fp8 (default yv7.graph.FP8_MIN_COUT; 0 = all of them)."""
+    @classmethod
+    def fp8_scales(cls, model, device, calib=None, min_cout=None):
+        """{op index: activation scale} of the fp8 plan's e4m3 convs, from calibration: the fp16 plan runs
+        `calib` ([B,3,H,W] frames in [0,1]; default: 2 seeded synthetic frames at the model's native size)
+        and each fp8 op's input amax sets xscale = 2**ceil(log2(amax / 448)), so the largest calibrated
+        value still fits e4m3.  min_cout: which eligible 1x1 convs go fp8 (default
+        yv7.graph.FP8_MIN_COUT; 0 = all of them)."""
         from yv7.graph import FP8_MIN_COUT, fp8_candidates
         min_cout = FP8_MIN_COUT if min_cout is None else min_cout
         base = cls.from_model(model, device, torch.float16)
@@ -151,9 +157,8 @@ class Plan:
             v = base.tensor_view(o['src'], B, H, W)[..., o['src_coff']:o['src_coff'] + o['cin']]
             amax = float(v.abs().max().float())
             scales[i] = 2.0 ** math.ceil(math.log2(amax / 448.0)) if amax > 0 else 1.0
-        g = compile_model(model, L.DT_F16, fp8=scales)
         del base
-        return cls(g, device, g.weight_blob().to(device))
+        return scales
 
     def __del__(self):
         self._ws = {}
