@@ -123,10 +123,10 @@ int main(int argc, char** argv) {
     for (int n = 0; n < s.cout; ++n)
       hipLaunchKernelGGL(fill_rand, dim3(4), dim3(256), 0, 0, w + (size_t)n * p.kpad, (size_t)p.K, 7u + n,
                          1.0f / sqrtf((float)p.K));
-    if (s.k == 3 && s.cin % 32 == 0) {
-      CK(yv7::pack_frag3x3(w, p.kpad, s.cin, s.cout, wf, 0));
+    if (s.cin % 32 == 0) {
+      CK(yv7::pack_frag(w, p.kpad, s.cin, s.cout, s.k * s.k, wf, 0));
       p.wf = wf;
-      p.wfbytes = (uint32_t)yv7::frag3x3_bytes(s.cin, s.cout);
+      p.wfbytes = (uint32_t)yv7::frag_bytes(s.cin, s.cout, s.k * s.k);
     }
     const size_t ny = yv7::bordered_pixels(s.B, p.Ho, p.Wo) * s.cout;
     double flops = 2.0 * p.M * s.cout * p.K;

@@ -28,7 +28,8 @@ DEV = 'cuda:0'
 
 CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15,
                  100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
-                 201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274]
+                 201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274, 275, 276,
+                 280, 281, 282, 283, 284]
 DET_VARIANTS = [92, 97, 99]
 
 
@@ -67,7 +68,7 @@ def test_variant_api_rejects_hooks():
     plan = m.plan()
     conv = next(i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV)
     for v in (12, 13, 14, 16, 17, 18, 19, 90, 91, 93, 94, 298, 160, 105, 211, 221, 233, 237, 238, 240, 241,
-              248, 255, 259, 260, 261, 263, 275, 911):
+              248, 255, 259, 260, 261, 263, 277, 285, 911):
         with pytest.raises(RuntimeError):
             plan.set_op_variant(conv, v)
     with pytest.raises(RuntimeError):

@@ -130,16 +130,21 @@ __global__ __launch_bounds__(NT) void copy_kernel(const T* __restrict__ x, int B
 
 // ---- SPPCSPC pool cascade (common.py:271, 276-280 with k = (5, 9, 13)): the three stride-1 pools
 //      p5 = pool5(x), p9 = pool5(p5), p13 = pool5(p9) (max is associative; -inf padding keeps the
-//      cascade exact) in one launch.  Block = one image x 16 channels: the whole H x W x 16 plane is
+//      cascade exact) in one launch.  Block = one image x SPP_CG channels (fp16: 64 = one 128-byte
+//      line per pixel, so every global load and store covers whole lines): the H x W x CG plane is
 //      staged in LDS once; each 5 x 5 pool runs separably (a 5-wide row max into a scratch plane, then
-//      a 5-tall column max: 10 LDS reads per output instead of 25; taps outside the image re-read the
-//      centre, max being idempotent = the -inf padding), ping-ponging between two planes; every
-//      stage's output also leaves as 16-byte stores into its concat slice.
-constexpr int SPP_CG = 16;
+//      a 5-tall column max written back over the stage's input plane, which the row pass has finished
+//      reading: 10 LDS reads per output instead of 25; taps outside the image re-read the centre, max
+//      being idempotent = the -inf padding); every stage's output also leaves as 16-byte stores into
+//      its concat slice.  Round 3's form (16 channels per block: a pixel's 32 bytes per store, a
+//      quarter of a line) took 34 us for yolov7's 20 x 20 x 512 at bs 32 — write-combining of partial
+//      lines, not bandwidth (52 MB).
+constexpr int SPP_CG = 64;
+constexpr int SPP_NT = 512;
 
 template <typename T>
-__global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x, int B, int H, int W, int xc,
-                                                         int coff, int C, T* __restrict__ y) {
+__global__ __launch_bounds__(SPP_NT) void spp_cascade_kernel(const T* __restrict__ x, int B, int H, int W, int xc,
+                                                             int coff, int C, T* __restrict__ y) {
   constexpr int V = Vec<T>::N;
   constexpr int CG = SPP_CG;             // channels per block
   constexpr int NCH = CG / V;            // 16-byte chunks per pixel
@@ -147,12 +152,11 @@ __global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x
   const int groups = C / CG;
   const int b = blockIdx.x / groups, c0 = (blockIdx.x - b * groups) * CG;
   const int npx = H * W, items = npx * NCH;
-  u4* buf0 = reinterpret_cast<u4*>(lds);
-  u4* buf1 = buf0 + items;
-  u4* tmp = buf1 + items;
-  for (int i = threadIdx.x; i < items; i += NT) {
+  u4* plane = reinterpret_cast<u4*>(lds);
+  u4* tmp = plane + items;
+  for (int i = threadIdx.x; i < items; i += SPP_NT) {
     const int px = i / NCH, ch = i - px * NCH, h = px / W, w = px - h * W;
-    buf0[i] = *reinterpret_cast<const u4*>(x + pix_index(b, h, w, H, W) * xc + coff + c0 + ch * V);
+    plane[i] = *reinterpret_cast<const u4*>(x + pix_index(b, h, w, H, W) * xc + coff + c0 + ch * V);
   }
   __syncthreads();
   auto vmax = [](u4 a, u4 c) -> u4 {
@@ -164,22 +168,20 @@ __global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x
       return __builtin_bit_cast(u4, __builtin_elementwise_max(__builtin_bit_cast(fv4, a), __builtin_bit_cast(fv4, c)));
     }
   };
-  u4* src = buf0;
-  u4* dst = buf1;
   for (int stage = 1; stage <= 3; ++stage) {
-    for (int i = threadIdx.x; i < items; i += NT) {   // row max: 5 taps along w
+    for (int i = threadIdx.x; i < items; i += SPP_NT) {   // row max: 5 taps along w
       const int px = i / NCH, ch = i - px * NCH, w = px % W;
-      u4 m = src[i];
+      u4 m = plane[i];
 #pragma unroll
       for (int dx = -2; dx <= 2; ++dx) {
         if (dx == 0) continue;
         const bool in = (unsigned)(w + dx) < (unsigned)W;
-        m = vmax(m, src[(in ? px + dx : px) * NCH + ch]);
+        m = vmax(m, plane[(in ? px + dx : px) * NCH + ch]);
       }
       tmp[i] = m;
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < items; i += NT) {   // column max: 5 taps along h
+    for (int i = threadIdx.x; i < items; i += SPP_NT) {   // column max: 5 taps along h
       const int px = i / NCH, ch = i - px * NCH, h = px / W, w = px - h * W;
       u4 m = tmp[i];
 #pragma unroll
@@ -188,13 +190,10 @@ __global__ __launch_bounds__(NT) void spp_cascade_kernel(const T* __restrict__ x
         const bool in = (unsigned)(h + dy) < (unsigned)H;
         m = vmax(m, tmp[(in ? px + dy * W : px) * NCH + ch]);
       }
-      dst[i] = m;
+      plane[i] = m;
       *reinterpret_cast<u4*>(y + pix_index(b, h, w, H, W) * xc + coff + stage * C + c0 + ch * V) = m;
     }
     __syncthreads();
-    u4* t = src;
-    src = dst;
-    dst = t;
   }
 }
 
@@ -299,20 +298,27 @@ hipError_t launch_copy(int dtype, const void* x, int B, int H, int W, int xc, in
 
 bool spp_cascade_supported(int dtype, int H, int W, int C) {
   const int V = dtype == 1 ? 8 : 4;
-  return C % SPP_CG == 0 && (size_t)3 * H * W * (SPP_CG / V) * 16 <= 64 * 1024;
+  return C % SPP_CG == 0 && (size_t)2 * H * W * (SPP_CG / V) * 16 <= 160 * 1024;
 }
 
 // x: the concat tensor (pitch xc) holding the pool input at channel slice [coff, coff + C); the three
 // pools go to [coff + C, coff + 2C), [coff + 2C, coff + 3C), [coff + 3C, coff + 4C) of the same tensor.
 hipError_t launch_spp_cascade(int dtype, void* x, int B, int H, int W, int xc, int coff, int C, hipStream_t st) {
   const int V = dtype == 1 ? 8 : 4;
-  const size_t lds = (size_t)3 * H * W * (SPP_CG / V) * 16;
+  const size_t lds = (size_t)2 * H * W * (SPP_CG / V) * 16;
   const dim3 grid(B * (C / SPP_CG));
+  if (lds > 64 * 1024) {   // dynamic LDS past 64 KiB must be opted into per kernel
+    hipError_t e = dtype == 1 ? hipFuncSetAttribute((const void*)spp_cascade_kernel<_Float16>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds)
+                              : hipFuncSetAttribute((const void*)spp_cascade_kernel<float>,
+                                                    hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return e;
+  }
   if (dtype == 1)
-    YV7_LAUNCH(spp_cascade_kernel<_Float16>, grid, dim3(NT), lds, st, (const _Float16*)x, B, H, W, xc, coff, C,
+    YV7_LAUNCH(spp_cascade_kernel<_Float16>, grid, dim3(SPP_NT), lds, st, (const _Float16*)x, B, H, W, xc, coff, C,
                        (_Float16*)x);
   else
-    YV7_LAUNCH(spp_cascade_kernel<float>, grid, dim3(NT), lds, st, (const float*)x, B, H, W, xc, coff, C,
+    YV7_LAUNCH(spp_cascade_kernel<float>, grid, dim3(SPP_NT), lds, st, (const float*)x, B, H, W, xc, coff, C,
                        (float*)x);
   return hipGetLastError();
 }

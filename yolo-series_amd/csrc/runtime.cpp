@@ -41,7 +41,7 @@ struct yv7_plan {
   void* weights = nullptr;
   size_t wbytes = 0;
   void* zero = nullptr;  // 4 KiB of zeros
-  // fp16 plans: every 3x3 stride-1 conv's weights again, fragment-packed for conv_lr.hip (pack_frag3x3);
+  // fp16 plans: every 3x3 stride-1/2 and 1x1 stride-1 conv's weights again, fragment-packed for conv_lr.hip (pack_frag);
   // wf_off[op] = byte offset into wfrag, -1 when the op has none
   void* wfrag = nullptr;
   std::vector<int64_t> wf_off;
@@ -113,10 +113,10 @@ int kpad_of(const yv7_op_desc& o) {
   return (o.k * o.k * o.cin + 63) / 64 * 64;
 }
 bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7_WFMT_FP8; }
-// 3x3 / stride-1 or 2 / pad-1 fp16 convs get a fragment-packed weight copy (conv_lr.hip)
+// 3x3 / stride-1 or 2 / pad-1 and 1x1 / stride-1 fp16 convs get a fragment-packed weight copy (conv_lr.hip)
 bool wants_frag(int dtype, const yv7_op_desc& o) {
-  return dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && o.k == 3 && (o.s == 1 || o.s == 2) && o.pad == 1 && !o.pool &&
-         o.cin % 32 == 0;
+  const bool k3 = o.k == 3 && (o.s == 1 || o.s == 2) && o.pad == 1, k1 = o.k == 1 && o.s == 1 && o.pad == 0;
+  return dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && (k3 || k1) && !o.pool && o.cin % 32 == 0;
 }
 
 // Geometry / operand fields of a CONV or DETECT op's kernel parameters (pointers into the workspace
@@ -149,7 +149,7 @@ yv7::ConvParams conv_params(const yv7_plan* p, size_t op, int B, int H, int W) {
   c.variant = p->op_variant[op];
   if (p->wfrag && p->wf_off[op] >= 0) {
     c.wf = reinterpret_cast<const unsigned char*>(p->wfrag) + p->wf_off[op];
-    c.wfbytes = (uint32_t)yv7::frag3x3_bytes(o.cin, o.cout);
+    c.wfbytes = (uint32_t)yv7::frag_bytes(o.cin, o.cout, o.k * o.k);
   }
   return c;
 }
@@ -298,15 +298,15 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
   for (size_t i = 0; i < p->ops.size(); ++i)
     if (wants_frag(p->dtype, p->ops[i])) {
       p->wf_off[i] = (int64_t)wf_total;
-      wf_total = align256(wf_total + yv7::frag3x3_bytes(p->ops[i].cin, p->ops[i].cout));
+      wf_total = align256(wf_total + yv7::frag_bytes(p->ops[i].cin, p->ops[i].cout, p->ops[i].k * p->ops[i].k));
     }
   if (wf_total) {
     e = hipMalloc(&p->wfrag, wf_total);
     for (size_t i = 0; e == hipSuccess && i < p->ops.size(); ++i)
       if (p->wf_off[i] >= 0)
-        e = yv7::pack_frag3x3(reinterpret_cast<const unsigned char*>(p->weights) + p->ops[i].w_off, kpad_of(p->ops[i]),
-                              p->ops[i].cin, p->ops[i].cout, reinterpret_cast<unsigned char*>(p->wfrag) + p->wf_off[i],
-                              nullptr);
+        e = yv7::pack_frag(reinterpret_cast<const unsigned char*>(p->weights) + p->ops[i].w_off, kpad_of(p->ops[i]),
+                           p->ops[i].cin, p->ops[i].cout, p->ops[i].k * p->ops[i].k,
+                           reinterpret_cast<unsigned char*>(p->wfrag) + p->wf_off[i], nullptr);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) {
       yv7_plan_destroy(p);
@@ -399,7 +399,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
   return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
-         (v >= 270 && v <= 274);
+         (v >= 270 && v <= 276) || (v >= 280 && v <= 284);
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {
