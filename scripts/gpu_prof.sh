@@ -1,11 +1,11 @@
 #!/bin/bash
-# Round 3 profiles of the CURRENT tree (bench config yolov7 640 bs32 f16): the rocprofv3 kernel trace of
+# Per-round profiles of the CURRENT tree (bench config yolov7 640 bs32 f16): the rocprofv3 kernel trace of
 # serial forwards (the roofline's per-kernel launch times), the per-kernel HBM traffic (FETCH_SIZE /
 # WRITE_SIZE in separate --pmc passes), then the default bench line and its own kernel trace.
-# usage: bash scripts/gpu_r3_prof.sh TAG TREE
+# usage: bash scripts/gpu_prof.sh TAG TREE   (TAG r4 writes profiles/r4_pmc_traffic.json, which bench.py reads)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-TAG=${1:-r3}; TREE=${2:-}
+TAG=${1:-r4}; TREE=${2:-}
 O=gpurun_out/$TAG
 cd $R && mkdir -p $O
 export PYTHONPATH=$R/yolo-series_amd:$R

@@ -1,5 +1,5 @@
 """Per-kernel HBM traffic from rocprofv3 PMC passes (FETCH_SIZE and WRITE_SIZE in separate runs of the
-same serial workload, scripts/gpu_r3_prof.sh), keyed by kernel instantiation exactly as bench.py
+same serial workload, scripts/gpu_prof.sh), keyed by kernel instantiation exactly as bench.py
 groups its per-op timings (yv7.runtime.kernel_key of the names yv7_op_kernels reports).
 
 gfx950 corrections (MI355X_MICROARCH.md, HBM section): read bytes = 2 x FETCH_SIZE (64 B counted per

@@ -2033,8 +2033,6 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // no layer in the checked networks
   if (!det && (variant == 262 || (variant >= 911 && variant <= 914)) && hring_supported(p) && p.cout % 128 == 0)
     return launch_conv_hring(p, device_cus(), st);
-  // the low-resolution kernel's 1x1 form (conv_lr.hip): 280 + tile configuration
-  if (!det && variant >= 280 && variant <= 284 && lr1_supported(p, variant - 280)) return launch_conv1x1_lr(p, variant - 280, st);
   // the low-resolution 3x3 kernel (conv_lr.hip): 270 + tile configuration
   if (!det && variant >= 270 && variant <= 276 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
   // 3x3 stride-1 layers of up to 204 800 output pixels (yolov7 640 bs 32 from 80^2 down, yolov7-w6 1280
@@ -2052,7 +2050,17 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
       !((long)p.B * (p.H / 16) * (p.W / 16) >= 2048 && ws64_supported(p))) {
     const bool t5 = p.H % 5 == 0;
     const long t128 = (long)((p.B + 3) / 4) * (p.H / (t5 ? 5 : 4)) * (p.W / 4) * (p.cout / 128);
-    const int cfg = (p.cout % 128 == 0 && t128 >= 400 ? 0 : 1) + (t5 ? 0 : 2);
+    int cfg = (p.cout % 128 == 0 && t128 >= 400 ? 0 : 1) + (t5 ? 0 : 2);
+    // 160-pixel tiles (10 rows: each weight fragment feeds twice the MFMAs) where they keep >= 400 / 640
+    // blocks (profiles/r4lr/tune_tm10*.txt, us): 160 x 128 for the channel-doubling RepConvs up to 384
+    // inputs (yolov7 128->256 @80 115.5 -> 111.9, 256->512 @40 105.9 -> 100.2; w6 256->512 @80 104.2 ->
+    // 95.9, 384->768 @40 62.2 -> 56.7), 160 x 64 for the other wide / 64-channel layers (512->512 @20
+    // 61.9 -> 57.4, 512->1024 @20 103.8 -> 99.3, 128->64 @80 40.5 -> 37.7, 256->256 @40 56.3 -> 54.9)
+    if (p.H % 10 == 0) {
+      const long g10 = (long)((p.B + 3) / 4) * (p.H / 10) * (p.W / 4);
+      if (p.cout % 128 == 0 && p.cout >= 2 * p.cin && p.cin <= 384 && g10 * (p.cout / 128) >= 400) cfg = 5;
+      else if (p.cout != 128 && p.cout % 64 == 0 && g10 * (p.cout / 64) >= 640) cfg = 6;
+    }
     if (lr_supported(p, cfg)) return launch_conv_lr(p, cfg, st);
   }
   // 3x3 stride-2 layers the 128 x 128 ring would split K for (under 256 of its tiles: yolov7's 256->256

@@ -118,15 +118,17 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
   // ---- weight fragments: (nf, chunk, tap) at ((nf * NCH + c) * 9 + tap) KiB, lane-linear
   const int nf0 = n0 / 16 + wn * TN;
   u4 wreg[NWB][3][TN];
+  uint32_t wlane[TN];   // the lane's offset in the first fragment of each of its channel groups
+#pragma unroll
+  for (int j = 0; j < TN; ++j) wlane[j] = (uint32_t)((nf0 + j) * NCH * 9 * 1024 + lane * 16);
   auto load_w = [&](int ph, u4 (&w)[3][TN]) __attribute__((always_inline)) {
     const int c = ph / 3, s = ph % 3;
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
-      for (int j = 0; j < TN; ++j)
-        w[r][j] = __builtin_bit_cast(
-            u4, __builtin_amdgcn_raw_buffer_load_b128(
-                    wr, (uint32_t)((((nf0 + j) * NCH + c) * 9 + r * 3 + s) * 1024 + lane * 16), 0, 0));
+      for (int j = 0; j < TN; ++j)   // (chunk, tap) as the scalar offset: no per-load address VALU
+        w[r][j] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(
+                                             wr, wlane[j], (uint32_t)((c * 9 + r * 3 + s) * 1024), 0));
   };
 
   // ---- accumulators: bias
@@ -155,26 +157,33 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
   if constexpr (NCH > 1) load_patch(1);
   __syncthreads();
 
+  // patch rows of column step (c, s): the lane's column 2x + s (S = 2) or x + s sits in slot
+  // x + col_slot(s) - col_slot(0)
+  auto read_xa = [&](int c, int s, u4 (&xa)[NXA]) __attribute__((always_inline)) {
+    const unsigned char* pb = smem + (c & 1) * PB + a_wave + a_lane + col_slot<S>(s) * 64;
+#pragma unroll
+    for (int j = 0; j < NXA; ++j) xa[j] = *reinterpret_cast<const u4*>(pb + j * PC * 64);
+  };
+  auto mfmas = [&](int ph, const u4 (&xa)[NXA]) __attribute__((always_inline)) {
+    const u4(&w)[3][TN] = wreg[ph % NWB];
+#pragma unroll
+    for (int r = 0; r < 3; ++r)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w[r][j]),
+                                                             __builtin_bit_cast(h8, xa[S * i + r]), acc[j][i], 0, 0, 0);
+  };
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
       const int ph = c * 3 + s;
       if (ph + PD < NPH) load_w(ph + PD, wreg[(ph + PD) % NWB]);
-      // the lane's column 2x + s (S = 2) or x + s sits in slot x + col_slot(s) - col_slot(0)
-      const unsigned char* pb = smem + (c & 1) * PB + a_wave + a_lane + col_slot<S>(s) * 64;
       u4 xa[NXA];
-#pragma unroll
-      for (int j = 0; j < NXA; ++j) xa[j] = *reinterpret_cast<const u4*>(pb + j * PC * 64);
-      const u4(&w)[3][TN] = wreg[ph % NWB];
-#pragma unroll
-      for (int r = 0; r < 3; ++r)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int i = 0; i < TM; ++i)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w[r][j]),
-                                                               __builtin_bit_cast(h8, xa[S * i + r]), acc[j][i], 0, 0, 0);
+      read_xa(c, s, xa);
+      mfmas(ph, xa);
     }
     if (c + 1 < NCH) {
       store_patch((c + 1) & 1);   // buffer of chunk c - 1: every wave left it at the last barrier
@@ -241,158 +250,6 @@ __global__ void pack_frag_kernel(const _Float16* w, int kpad, int cin, int nfrag
   }
 }
 
-// ---------------------------------------------------------------------------------------------------
-// 1x1 / stride-1 convs (Conv.fuseforward with k = 1, common.py:110-111: a GEMM of M pixels x K = cin x
-// N = cout) in the same form: BM = 16 * TM * WM consecutive output pixels (any 16 consecutive pixels
-// are one MFMA fragment for a 1x1) x BN = 16 * TN * WN channels per block; per stage of KC 32-channel
-// chunks the block's A tile (BM pixels x 32 KC channels) is register-staged into LDS once and read by
-// all WN channel waves, each wave streams its own weight fragments (fragment-packed, 1 KiB per
-// (16 channels, chunk)) into VGPRs one stage ahead; one barrier per stage.  Pixel tiles of 80 / 160
-// divide the bs-32 layers' 12 800 / 51 200 / 204 800 pixels, so a layer's tiles spread evenly over
-// the 256 CUs where the 256 x 256 tiles of the 8-phase ring leave 22 % of them idle on a last round.
-// LDS row = one pixel's KC * 64 bytes; 16-byte slot q of pixel px sits at q ^ (px & (slots - 1)),
-// conflict-free for the fragment reads (16 consecutive pixels x 4 chunks per lane group, KC >= 2).
-template <int WM, int WN, int TN, int TM, int KC, int ACT>
-__global__ __launch_bounds__(64 * WM * WN) void conv1x1_lr_kernel(const ConvParams p) {
-  constexpr int NT = 64 * WM * WN, BM = 16 * TM * WM, BN = 16 * TN * WN;
-  constexpr int RB = KC * 64, NS = RB / 16, SB = BM * RB;
-  constexpr int NPL = (BM * NS + NT - 1) / NT;
-  static_assert(KC >= 2 && (NS & (NS - 1)) == 0, "swizzle needs >= 8 power-of-two slots per row");
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * SB];
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int g = lane >> 4, li = lane & 15;
-  const int G = gridDim.x, bid = blockIdx.x;
-  const int t = (G % 8 == 0) ? (bid % 8) * (G / 8) + bid / 8 : bid;
-  const int nN = (p.cout + BN - 1) / BN;
-  const int n0 = (t % nN) * BN, m0 = (t / nN) * BM;
-  const int HW = p.H * p.W;
-  const int nst = p.cin / (CK * KC);
-  const int nch = p.cin / CK;
-
-  const auto xr = make_rsrc(p.x, p.xbytes);
-  const auto wr = make_rsrc(p.wf, p.wfbytes);
-  const auto yr = make_rsrc(p.y, 0x7fffffffu);
-
-  uint32_t po[NPL], pd[NPL];
-#pragma unroll
-  for (int k = 0; k < NPL; ++k) {
-    const int q = tid + k * NT;
-    const int px = q / NS, sl = q % NS, m = m0 + px;
-    if (q < BM * NS && m < p.M) {
-      const int b = m / HW, r = m - b * HW, y = r / p.W, x = r - y * p.W;
-      po[k] = (uint32_t)((pix_index(b, y, x, p.H, p.W) * p.xc + p.xoff + sl * 8) * 2);
-    } else {
-      po[k] = OOB;
-    }
-    pd[k] = q < BM * NS ? (uint32_t)(px * RB + ((sl ^ (px & (NS - 1))) * 16)) : 0xffffffffu;
-  }
-  u4 pr[NPL];
-  auto load_a = [&](int st) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < NPL; ++k)
-      pr[k] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, po[k], (uint32_t)(st * RB), 0));
-  };
-  auto store_a = [&](int buf) __attribute__((always_inline)) {
-#pragma unroll
-    for (int k = 0; k < NPL; ++k)
-      if (pd[k] != 0xffffffffu) *reinterpret_cast<u4*>(smem + buf * SB + pd[k]) = pr[k];
-  };
-  const int nf0 = n0 / 16 + wn * TN;
-  u4 w0[KC][TN], w1[KC][TN];
-  auto load_w = [&](int st, u4 (&w)[KC][TN]) __attribute__((always_inline)) {
-#pragma unroll
-    for (int c = 0; c < KC; ++c)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-        w[c][j] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(
-                                             wr, (uint32_t)(((nf0 + j) * nch + st * KC + c) * 1024 + lane * 16), 0, 0));
-  };
-
-  f4 acc[TN][TM];
-#pragma unroll
-  for (int j = 0; j < TN; ++j) {
-    const int col = n0 + wn * TN * 16 + j * 16 + g * 4;
-    f4 bv;
-#pragma unroll
-    for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
-#pragma unroll
-    for (int i = 0; i < TM; ++i) acc[j][i] = bv;
-  }
-  // fragment read offsets: pixel row wm*TM*16 + i*16 + li, slot c*4 + g (swizzled by the row)
-  const int row0 = wm * TM * 16 + li;
-
-  load_a(0);
-  load_w(0, w0);
-  store_a(0);
-  __syncthreads();
-  // stage s: next stage's A and weights in flight during this stage's MFMAs
-  auto stage = [&](int st, auto par, u4 (&w)[KC][TN], u4 (&wn_)[KC][TN]) __attribute__((always_inline)) {
-    constexpr int PAR = decltype(par)::value;
-    const bool more = st + 1 < nst;
-    if (more) {
-      load_a(st + 1);
-      load_w(st + 1, wn_);
-    }
-    const unsigned char* ab = smem + PAR * SB;
-#pragma unroll
-    for (int c = 0; c < KC; ++c) {
-      u4 xa[TM];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) {
-        const int row = row0 + i * 16;
-        xa[i] = *reinterpret_cast<const u4*>(ab + row * RB + (((c * 4 + g) ^ (row & (NS - 1))) * 16));
-      }
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int i = 0; i < TM; ++i)
-          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, w[c][j]), __builtin_bit_cast(h8, xa[i]),
-                                                             acc[j][i], 0, 0, 0);
-    }
-    if (more) {
-      store_a(PAR ^ 1);   // the other buffer: every wave left it at the last barrier
-      __syncthreads();
-    }
-  };
-  for (int st = 0; st < nst; st += 2) {
-    stage(st, std::integral_constant<int, 0>{}, w0, w1);
-    if (st + 1 < nst) stage(st + 1, std::integral_constant<int, 1>{}, w1, w0);
-  }
-
-  // epilogue: pixel m0 + wm*TM*16 + i*16 + li, channels of lane g
-#pragma unroll
-  for (int i = 0; i < TM; ++i) {
-    const int m = m0 + row0 + i * 16;
-    const bool live = m < p.M;
-    uint32_t yo = 0x80000000u;
-    if (live) {
-      const int b = m / HW, r = m - b * HW, y = r / p.W, x = r - y * p.W;
-      yo = (uint32_t)((pix_index(b, y, x, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
-    }
-    typedef _Float16 h4 __attribute__((ext_vector_type(4)));
-    typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-    const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
-#pragma unroll
-    for (int mp = 0; mp < TN / 2; ++mp) {
-      h4 va, vb;
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        va[e] = (_Float16)act_t<ACT>(acc[2 * mp][i][e]);
-        vb[e] = (_Float16)act_t<ACT>(acc[2 * mp + 1][i][e]);
-      }
-      const u2 a = __builtin_bit_cast(u2, va), b = __builtin_bit_cast(u2, vb);
-      const auto s0 = __builtin_amdgcn_permlane16_swap(a[0], b[0], false, false);
-      const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
-      const u4 v = {s0[0], s1[0], s0[1], s1[1]};
-      const int n = n0 + wn * TN * 16 + mp * 32 + (int)lane_ch;
-      __builtin_amdgcn_raw_buffer_store_b128(v, yr, (live && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu, 0, 0);
-    }
-  }
-}
-
 template <int WM, int WN, int TN, int TM, int PD, int S, int NCH>
 hipError_t launch_cfg(const ConvParams& p, hipStream_t st) {
   constexpr int TH = TM * WM, BN = WN * TN * 16;
@@ -426,8 +283,12 @@ hipError_t launch_nch(const ConvParams& p, hipStream_t st) {
 // 64 x 128.  At stride 2 the same four were correct but slower than the dispatch on the large yolov7
 // stride-2 layers (profiles/r4lr/convbench_s2.txt: 64->128 s2 @320 243 vs 215 us, 256->256 s2 @80 77
 // vs 68: a 9-column, 2*TH+1-row patch per output tile is 4-5 input pixels per output against 2.1 at
-// stride 1) and faster only where the dispatch split K: 256->256 s2 @40 25.4 vs 29.6.
-#define LR_CFGS(X) \
+// stride 1) and faster only where the dispatch split K: 256->256 s2 @40 25.4 vs 29.6.  5 / 6: 160-pixel
+// tiles (TH = 10) of 128 / 64 channels (profiles/r4lr/tune_tm10*.txt: 3-9 % on the wide layers).
+// Reading the next column step's patch rows before this step's MFMAs (two register sets; across a
+// chunk boundary after the barrier) was no faster on any layer and cost a wave per SIMD
+// (profiles/r4lr/tune_xp.txt): three waves per SIMD already hide the LDS latency.
+#define LR_CFGS(X)                                                                                   \
   X(0, 1, 4, 2, 5, 3, 1) X(1, 1, 4, 1, 5, 3, 1) X(2, 1, 4, 2, 4, 3, 1) X(3, 1, 4, 1, 4, 3, 1) X(4, 1, 4, 2, 4, 3, 2) \
   X(5, 1, 4, 2, 10, 2, 1) X(6, 1, 4, 1, 10, 3, 1)
 #define LR_ROW(i, wm, wn, tn, tm, pd, s) {wm, wn, tn, tm, pd, s},
@@ -465,41 +326,6 @@ hipError_t launch_conv_lr(const ConvParams& p, int cfg, hipStream_t st) {
   case i: return launch_nch<wm, wn, tn, tm, pd, s>(p, st);
     LR_CFGS(LR_CASE)
 #undef LR_CASE
-  }
-  return hipErrorInvalidValue;
-}
-
-// 1x1 configurations {WM, WN, TN, TM, KC} (variants 280 + row)
-#define LR1_CFGS(X) X(0, 1, 4, 2, 5, 2) X(1, 1, 4, 2, 5, 4) X(2, 1, 4, 2, 10, 2) X(3, 2, 2, 2, 5, 2) X(4, 1, 8, 2, 5, 2)
-#define LR1_ROW(i, wm, wn, tn, tm, kc) {wm, wn, tn, tm, kc},
-constexpr int LR1_CFG[][5] = {LR1_CFGS(LR1_ROW)};
-constexpr int LR1_NCFG = sizeof(LR1_CFG) / sizeof(LR1_CFG[0]);
-
-bool lr1_supported(const ConvParams& p, int cfg) {
-  if (cfg < 0 || cfg >= LR1_NCFG) return false;
-  const int BN = 16 * LR1_CFG[cfg][1] * LR1_CFG[cfg][2], KC = LR1_CFG[cfg][4];
-  return p.wf && p.k == 1 && p.s == 1 && p.pad == 0 && !p.pool && p.cin % (CK * KC) == 0 && p.cout % BN == 0 &&
-         p.Ho == p.H && p.Wo == p.W && p.xoff % 8 == 0 && p.xc % 8 == 0 && p.yoff % 8 == 0 && p.yc % 8 == 0 &&
-         (size_t)p.M * p.cin < ((size_t)1 << 31);
-}
-
-template <int WM, int WN, int TN, int TM, int KC>
-hipError_t launch_lr1(const ConvParams& p, hipStream_t st) {
-  constexpr int BM = 16 * TM * WM, BN = 16 * TN * WN;
-  const long T = (long)((p.M + BM - 1) / BM) * (p.cout / BN);
-  if (p.act == 1) YV7_LAUNCH((conv1x1_lr_kernel<WM, WN, TN, TM, KC, 1>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
-  else if (p.act == 2) YV7_LAUNCH((conv1x1_lr_kernel<WM, WN, TN, TM, KC, 2>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
-  else YV7_LAUNCH((conv1x1_lr_kernel<WM, WN, TN, TM, KC, 0>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
-  return hipGetLastError();
-}
-
-hipError_t launch_conv1x1_lr(const ConvParams& p, int cfg, hipStream_t st) {
-  if (!lr1_supported(p, cfg)) return hipErrorInvalidValue;
-  switch (cfg) {
-#define LR1_CASE(i, wm, wn, tn, tm, kc) \
-  case i: return launch_lr1<wm, wn, tn, tm, kc>(p, st);
-    LR1_CFGS(LR1_CASE)
-#undef LR1_CASE
   }
   return hipErrorInvalidValue;
 }

@@ -41,7 +41,7 @@ struct yv7_plan {
   void* weights = nullptr;
   size_t wbytes = 0;
   void* zero = nullptr;  // 4 KiB of zeros
-  // fp16 plans: every 3x3 stride-1/2 and 1x1 stride-1 conv's weights again, fragment-packed for conv_lr.hip (pack_frag);
+  // fp16 plans: every 3x3 stride-1/2 conv's weights again, fragment-packed for conv_lr.hip (pack_frag);
   // wf_off[op] = byte offset into wfrag, -1 when the op has none
   void* wfrag = nullptr;
   std::vector<int64_t> wf_off;
@@ -113,10 +113,10 @@ int kpad_of(const yv7_op_desc& o) {
   return (o.k * o.k * o.cin + 63) / 64 * 64;
 }
 bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7_WFMT_FP8; }
-// 3x3 / stride-1 or 2 / pad-1 and 1x1 / stride-1 fp16 convs get a fragment-packed weight copy (conv_lr.hip)
+// 3x3 / stride-1 or 2 / pad-1 fp16 convs get a fragment-packed weight copy (conv_lr.hip)
 bool wants_frag(int dtype, const yv7_op_desc& o) {
-  const bool k3 = o.k == 3 && (o.s == 1 || o.s == 2) && o.pad == 1, k1 = o.k == 1 && o.s == 1 && o.pad == 0;
-  return dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && (k3 || k1) && !o.pool && o.cin % 32 == 0;
+  return dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && o.k == 3 && (o.s == 1 || o.s == 2) &&
+         o.pad == 1 && !o.pool && o.cin % 32 == 0;
 }
 
 // Geometry / operand fields of a CONV or DETECT op's kernel parameters (pointers into the workspace
@@ -399,7 +399,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
   return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
-         (v >= 270 && v <= 276) || (v >= 280 && v <= 284);
+         (v >= 270 && v <= 276);
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {

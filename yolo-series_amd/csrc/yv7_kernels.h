@@ -142,8 +142,8 @@ struct ConvParams {
   int cnt_n;
   int ksplit;
   int pool;           // 2: 1x1 conv over the 2x2 / stride-2 max of the input (MP folded in; k = 1, s = 2)
-  // 3x3 stride-1/2 and 1x1 stride-1 convs of fp16 plans: the weights again, fragment-packed for
-  // conv_lr.hip (pack_frag), or null
+  // 3x3 stride-1/2 convs of fp16 plans: the weights again, fragment-packed for conv_lr.hip (pack_frag),
+  // or null
   const void* wf;
   uint32_t wfbytes;
 };
@@ -210,9 +210,6 @@ bool hring_supported(const ConvParams& p);
 // low-resolution 3x3 (conv_lr.hip): cfg 0-4 = tile shape; weights from ConvParams::wf
 bool lr_supported(const ConvParams& p, int cfg);
 hipError_t launch_conv_lr(const ConvParams& p, int cfg, hipStream_t st);
-// its 1x1 form: cfg 0-4; weights from ConvParams::wf (packed with taps = 1)
-bool lr1_supported(const ConvParams& p, int cfg);
-hipError_t launch_conv1x1_lr(const ConvParams& p, int cfg, hipStream_t st);
 size_t frag_bytes(int cin, int cout, int taps);
 hipError_t pack_frag(const void* w, int kpad, int cin, int cout, int taps, void* out, hipStream_t st);
 hipError_t launch_conv_hring(const ConvParams& p, int cus, hipStream_t st);
