@@ -3,7 +3,7 @@
 # [3] yolov7-w6 1280 bs8 f16, [4] yolov7 640 bs32 fp8 1x1, and yolov7-tiny 640 bs32.
 set -o pipefail
 R=$GRAFT_REPO_ROOT
-TAG=${1:-r3lines}
+TAG=${1:-r4lines}
 O=gpurun_out/$TAG
 cd $R && mkdir -p $O
 export PYTHONPATH=$R/yolo-series_amd:$R
@@ -13,3 +13,6 @@ run() {   # name, args...
   python -c "import json;d=json.load(open('$O/$n.json'));print('$n', d['value'], d['unit'], d['config'].get('workload'))"
 }
 run f16 && run w6 --model yolov7-w6 --img 1280 --batch 8 && run fp8 --dtype fp8 && run tiny --model yolov7-tiny && run f16b
+# batches in flight on the current kernels (round 4): 2 and 4 streams beside the default 3
+[ -n "$STREAMS_AB" ] && run s2 --streams 2 && run s4 --streams 4
+true
