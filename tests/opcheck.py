@@ -117,8 +117,11 @@ def check_ops(plan, x, B, H, W, raw=None, z=None, skip_fp8=True):
             # csrc/stem.hip's arithmetic: with SiLU on both convs, conv A's weights / bias are
             # pre-scaled by -log2(e) (weights rounded to fp16 again), A is stored in fp16 as
             # -log2(e) * silu(a), conv B's bias is scaled the same way and its epilogue undoes it
-            xin = x.to(es_dt).float().permute(0, 2, 3, 1).contiguous()
-            wa, ba = _weights(plan, blob, dict(o, cin=3))
+            reorg = o['cin'] == 12   # the w6 front end: ReOrg (common.py:52-53) + conv A on 12 channels
+            xr = torch.cat([x[..., ::2, ::2], x[..., 1::2, ::2], x[..., ::2, 1::2], x[..., 1::2, 1::2]], 1) if reorg else x
+            xin = xr.to(es_dt).float().permute(0, 2, 3, 1).contiguous()
+            wa, ba = _weights(plan, blob, dict(o, cin=16 if reorg else 3))
+            wa = wa[..., :o['cin']]
             ob = dict(o, cin=o['cout'], cout=o['cout2'], w_off=o['w2_off'], b_off=o['b2_off'])
             wb, bb = _weights(plan, blob, ob)
             if o['act'] == L.ACT_SILU and o['act2'] == L.ACT_SILU:

@@ -58,8 +58,13 @@ def run(g, x: torch.Tensor, return_tensors=False):
                 v = torch.cat([v[..., ::2, ::2], v[..., 1::2, ::2], v[..., ::2, 1::2], v[..., 1::2, 1::2]], 1)
             T[o['dst']][:, :v.shape[1]] = v
         elif kind == L.OP_STEM:
-            wa = _weights(blob, g.dtype, o['w_off'], o['cout'], 3, 3)
-            a = _act(F.conv2d(x.float(), wa, _bias(blob, o['b_off'], o['cout']), o['s'], 1), o['act'])
+            v = x.float()
+            if o['cin'] == 12:   # the w6 front end: ReOrg fused (conv A's K packed as tap * 16 + ci)
+                v = torch.cat([v[..., ::2, ::2], v[..., 1::2, ::2], v[..., ::2, 1::2], v[..., 1::2, 1::2]], 1)
+                wa = _weights(blob, g.dtype, o['w_off'], o['cout'], 3, 16)[:, :12]
+            else:
+                wa = _weights(blob, g.dtype, o['w_off'], o['cout'], 3, 3)
+            a = _act(F.conv2d(v, wa, _bias(blob, o['b_off'], o['cout']), o['s'], 1), o['act'])
             wb = _weights(blob, g.dtype, o['w2_off'], o['cout2'], 3, o['cout'])
             y = _act(F.conv2d(a, wb, _bias(blob, o['b2_off'], o['cout2']), 2, 1), o['act2'])
             T[o['dst']][:, o['dst_coff']:o['dst_coff'] + o['cout2']] = y

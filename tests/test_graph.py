@@ -19,8 +19,8 @@ def test_compile_structure(name, dtype):
     assert kinds[L.OP_INPUT] + kinds[L.OP_STEM] == 1 and kinds[L.OP_DETECT] == g.nl
     assert kinds[L.OP_COPY] == 0          # every concat of the yolov7 family is written in place
     assert g.ops[0]['kind'] in (L.OP_INPUT, L.OP_STEM)
-    # the fused stem is used exactly for the fp16 plans of the P5 models (not for w6: ReOrg front end)
-    assert (kinds[L.OP_STEM] == 1) == (dtype == L.DT_F16 and 'w6' not in name)
+    # the fused stem is used exactly for the fp16 plans (w6: ReOrg + its two convs, stem_reorg_kernel)
+    assert (kinds[L.OP_STEM] == 1) == (dtype == L.DT_F16)
     for c, s in g.tensors:
         assert c % V == 0 and 0 <= s <= g.max_shift
     for o in g.ops:

@@ -241,7 +241,9 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
       if (d->dtype != YV7_DT_F16 || !yv7::stem_supported(o.cin, o.cout, o.cout2, o.s) || o.k != 3 || o.act != o.act2 ||
           o.dst_coff % vec || o.dst_coff + o.cout2 > d->tensors[o.dst].channels)
         return fail(YV7_E_ARG, "yv7_plan_create: unsupported stem op");
-      const size_t wa = (size_t)o.cout * ((27 + 63) / 64 * 64) * 2, wb = (size_t)o.cout2 * ((9 * o.cout + 63) / 64 * 64) * 2;
+      // cin 12: the w6 front end (ReOrg fused), conv A's K = tap * 16 + ci
+      const int ka = o.cin == 12 ? 9 * 16 : 27;
+      const size_t wa = (size_t)o.cout * ((ka + 63) / 64 * 64) * 2, wb = (size_t)o.cout2 * ((9 * o.cout + 63) / 64 * 64) * 2;
       if (o.w_off < 0 || o.w2_off < 0 || (size_t)o.w_off + wa > nbytes || (size_t)o.w2_off + wb > nbytes ||
           (size_t)o.b_off + 4 * o.cout > nbytes || (size_t)o.b2_off + 4 * o.cout2 > nbytes)
         return fail(YV7_E_ARG, "yv7_plan_create: stem weight range outside blob");
@@ -654,7 +656,9 @@ static int forward_impl(yv7_plan* p, const void* x, int x_dtype, int B, int H, i
       }
       case YV7_OP_STEM: {
         const auto& to = p->tensors[o.dst];
-        if ((H >> to.shift) != H / o.s / 2 || (W >> to.shift) != W / o.s / 2)
+        const int reorg = o.cin == 12;   // conv A runs on the 2x space-to-depth image
+        if ((H >> to.shift) != H / (reorg + 1) / o.s / 2 || (W >> to.shift) != W / (reorg + 1) / o.s / 2 ||
+            (reorg && (H % 4 || W % 4)))
           return fail(YV7_E_SHAPE, "yv7_forward: stem output shape mismatch");
         yv7::StemParams sp;
         sp.variant = 0;
@@ -669,7 +673,8 @@ static int forward_impl(yv7_plan* p, const void* x, int x_dtype, int B, int H, i
         sp.W = W;
         sp.yc = to.channels;
         sp.yoff = o.dst_coff;
-        sp.kpad_a = (27 + 63) / 64 * 64;
+        sp.reorg = reorg;
+        sp.kpad_a = ((reorg ? 9 * 16 : 27) + 63) / 64 * 64;
         sp.kpad_b = (9 * o.cout + 63) / 64 * 64;
         sp.act_a = o.act;
         sp.act_b = o.act2;

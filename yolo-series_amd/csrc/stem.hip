@@ -589,6 +589,319 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
   store_prev();
 }
 
+// The yolov7-w6 front end: ReOrg (space-to-depth 2x, models/common.py:48-53) + conv A (12 -> 64, 3x3,
+// stride 1, on the 640^2 reorganised image) + conv B (64 -> 128, 3x3, stride 2), cfg/deploy/
+// yolov7-w6.yaml:14-16.  Unfused these are three launches (the reorg packing, 36 us, conv A, 241 us,
+// conv B, 190 us at 1280^2 bs 8) around conv A's output, the largest tensor of the network (8 x 640^2 x
+// 64 fp16 = 419 MB, written once and read back through L2 by the stride-2 conv).
+//
+// Fused, one persistent 512-thread block per CU walks tiles of 4 x 16 conv-B output pixels, with the
+// waves split by role (one of each on every SIMD) and one barrier per tile:
+//   * A waves (0-3), tile t + 1: conv A on the MFMA — 9 x 33 A-pixels (20 m-tiles, padded) x 64
+//     channels, K = 9 taps x 16 channels (two taps per 16x16x32 K step, the fifth half zero weights);
+//     wave w: all 64 channels of m-tiles w, w + 4, ... (each patch read feeds 4 MFMAs), its 4 x 5 weight
+//     fragments in registers; + bias + act,
+//     zeroed outside the image (conv B's padding) -> A tile [A-pixel][64] (144-byte pitch, conflict-free
+//     for conv B's stride-2 reads), double-buffered.  Then the patch of tile t + 2 (loaded into
+//     registers during the previous tile) is committed to LDS and tile t + 3's is loaded: 11 x 35
+//     reorganised pixels x 16 halves (12 channels + 4 zero), gathered straight from the NCHW image — one
+//     dword load per (row parity, channel) covers a pixel's two raw columns, i.e. reorganised channels
+//     q*3 + c for q = rp (even column) and rp + 2 (odd column); double-buffered.
+//   * B waves (4-7), tile t: conv B on the MFMA — wave w owns output channels [32 (w-4), +32) for all 64
+//     pixels, its 2 x 18 weight fragments in registers; + bias + act -> the wave's own staging rows ->
+//     16-byte stores into the destination slice (no cross-wave exchange, so no barrier).
+// The A waves' SiLU (64 x 297 values per tile) and the B waves' MFMAs (576 per tile) thus issue side by
+// side on each SIMD instead of in turn behind barriers (the 4-wave form, one role after the other with
+// three barriers per tile: 360 vs 313... us, scripts/stembench.hip).
+// Arithmetic as stem2_kernel's: with SiLU, conv A's weights / bias pre-scaled by -log2(e) and its
+// activations stored in fp16 as -log2(e) silu(a) (tests/opcheck.py restates it); fp32 accumulation.
+constexpr int NT_RG = 512;
+
+template <typename S, int ACT_A, int ACT_B>
+__global__ __launch_bounds__(NT_RG, 1) void stem_reorg_kernel(const StemParams p) {
+  constexpr int CA = 64, CB = 128, TBY = 4, TBX = 16;
+  constexpr int TAY = 2 * TBY + 1, TAX = 2 * TBX + 1;   // conv-A pixels feeding the tile: 9 x 33
+  constexpr int NA = TAY * TAX;                          // 297
+  constexpr int MA = 20;                                 // conv-A m-tiles (padded)
+  constexpr int PY = TAY + 2, PX = TAX + 2, NPIX = PY * PX;   // reorganised patch 11 x 35
+  constexpr int APITCH = CA * 2 + 16;
+  constexpr int PATCH = NPIX * 32;
+  constexpr int ABUF = MA * 16 * APITCH;
+  constexpr int SPITCH = 32 * 2 + 16;                    // a B wave's staging row: 32 channels
+  constexpr int STG = TBY * TBX * SPITCH;
+  static_assert(MA * 16 >= NA, "conv A's m-tiles cover the A pixels");
+  static_assert(2 * PATCH + 2 * ABUF + 4 * STG <= 160 * 1024, "LDS");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PATCH + 2 * ABUF + 4 * STG];
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int HA = p.H / 2, WA = p.W / 2;            // the reorganised image = conv A's output grid
+  const int HB = HA / 2, WB = WA / 2;
+  const int tiles_x = (WB + TBX - 1) / TBX, tiles_y = (HB + TBY - 1) / TBY;
+  const int ntiles = p.B * tiles_x * tiles_y;
+  auto tile_geom = [&](int t, int& tb, int& ty, int& tx) {
+    tb = t / (tiles_x * tiles_y);
+    t -= tb * tiles_x * tiles_y;
+    ty = (t / tiles_x) * TBY;
+    tx = (t % tiles_x) * TBX;
+  };
+  // this block's tiles: vb, vb + G, ... (XCD-major virtual block index, as stem2_kernel)
+  const int G = gridDim.x;
+  const int vb = G % 8 == 0 ? (int)(blockIdx.x % 8) * (G / 8) + (int)(blockIdx.x / 8) : (int)blockIdx.x;
+  const int nmine = vb < ntiles ? (ntiles - vb + G - 1) / G : 0;
+  auto tile_of = [&](int i) { return vb + i * G; };
+
+  if (wave < 4) {
+    // ---------------- A waves: patches + conv A ----------------
+    const int w = wave;
+    // all 64 channels (4 n-tiles x 5 K steps of weight fragments) for m-tiles w, w + 4, ...: every patch
+    // read feeds 4 MFMAs.  SiLU folded as in stem2_kernel: weights and bias scaled by -log2(e) (weights
+    // rounded to fp16 again), so the MFMA yields z = -log2(e) a and the A tile holds z / (1 + 2^z) =
+    // -log2(e) silu(a); conv B's bias carries the same scale and its epilogue undoes it.
+    constexpr float NLOG2E = -1.4426950408889634f;
+    const float sa = ACT_A == 1 ? NLOG2E : 1.0f;
+    u4 wa[5][4];
+    f4 ba_l[4];
+#pragma unroll
+    for (int nt = 0; nt < 4; ++nt) {
+      const _Float16* wrow = reinterpret_cast<const _Float16*>(p.wa) + (size_t)(nt * 16 + li) * p.kpad_a + g * 8;
+#pragma unroll
+      for (int ks = 0; ks < 5; ++ks) {
+        h8 w8 = __builtin_bit_cast(h8, *reinterpret_cast<const u4*>(wrow + ks * 32));
+#pragma unroll
+        for (int e = 0; e < 8; ++e) w8[e] = (_Float16)((float)w8[e] * sa);
+        wa[ks][nt] = __builtin_bit_cast(u4, w8);
+      }
+      ba_l[nt] = *reinterpret_cast<const f4*>(p.ba + nt * 16 + g * 4) * sa;
+    }
+    // patch byte offset of this lane's tap in K step ks (tap 9 = none: tap 8's pixel against zero weights)
+    int toff[5];
+#pragma unroll
+    for (int ks = 0; ks < 5; ++ks) {
+      const int tap = min(2 * ks + (g >> 1), 8);
+      toff[ks] = ((tap / 3) * PX + tap % 3) * 32 + (g & 1) * 16;
+    }
+    // patch units = reorganised pixels, two per thread; unconditional buffer loads (outside the image: an
+    // offset past the buffer reads zero)
+    const int ta = tid;   // 0..255
+    constexpr int PPT = (NPIX + 255) / 256;
+    constexpr bool HALF = sizeof(S) == 2;
+    uint32_t pre[PPT][2][3];   // [unit][row parity][channel]: the two raw columns as packed halves
+    const uint32_t plane = (uint32_t)(p.H * p.W * sizeof(S));
+    const auto xr = make_rsrc(p.x, (uint32_t)((size_t)p.B * 3 * plane));
+    auto prefetch = [&](int t) {
+      int tb, ty, tx;
+      tile_geom(t, tb, ty, tx);
+      const int Y0 = 2 * ty - 2, X0 = 2 * tx - 2;   // patch origin on the reorganised grid
+      const uint32_t img = (uint32_t)tb * 3u * plane;
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) {
+        const int u = ta + k * 256;
+        const int py = u < NPIX ? u / PX : -0x40000, px = u - (u / PX) * PX;
+        const int Y = Y0 + py, X = X0 + px;
+        const bool in = (unsigned)Y < (unsigned)HA && (unsigned)X < (unsigned)WA && p.variant != 2;
+#pragma unroll
+        for (int rp = 0; rp < 2; ++rp) {
+          const uint32_t o = in ? img + (__umul24(2 * Y + rp, p.W) + 2 * X) * (uint32_t)sizeof(S) : 0x80000000u;
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            if constexpr (HALF) {
+              pre[k][rp][c] = __builtin_amdgcn_raw_buffer_load_b32(xr, o + c * plane, 0, 0);
+            } else {   // fp32 input: converted here (not the bench path)
+              typedef float f2 __attribute__((ext_vector_type(2)));
+              const f2 v = __builtin_bit_cast(f2, __builtin_amdgcn_raw_buffer_load_b64(xr, o + c * plane, 0, 0));
+              typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+              pre[k][rp][c] = __builtin_bit_cast(uint32_t, h2{(_Float16)v[0], (_Float16)v[1]});
+            }
+          }
+        }
+      }
+    };
+    auto commit = [&](unsigned char* patch) {
+      typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+      for (int k = 0; k < PPT; ++k) {
+        const int u = ta + k * 256;
+        _Float16 v[16];   // channel q * 3 + c, q = (row parity) + 2 (column parity)
+#pragma unroll
+        for (int rp = 0; rp < 2; ++rp)
+#pragma unroll
+          for (int c = 0; c < 3; ++c) {
+            asm volatile("" : "+v"(pre[k][rp][c]));
+            const h2 x2 = __builtin_bit_cast(h2, pre[k][rp][c]);
+            v[rp * 3 + c] = x2[0];
+            v[(rp + 2) * 3 + c] = x2[1];
+          }
+        h8 lo8, hi8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          lo8[e] = v[e];
+          hi8[e] = e < 4 ? v[8 + e] : (_Float16)0.f;
+        }
+        if (u < NPIX) {
+          *reinterpret_cast<u4*>(patch + u * 32) = __builtin_bit_cast(u4, lo8);
+          *reinterpret_cast<u4*>(patch + u * 32 + 16) = __builtin_bit_cast(u4, hi8);
+        }
+      }
+    };
+    auto conv_a = [&](int t, const unsigned char* patch, unsigned char* abuf) {
+      int tb, oy0, ox0;
+      tile_geom(t, tb, oy0, ox0);
+      const int ay0 = 2 * oy0 - 1, ax0 = 2 * ox0 - 1;
+#pragma unroll 1
+      for (int mt = w; mt < MA; mt += 4) {
+        const int m = mt * 16 + li;
+        const int mc = m < NA ? m : NA - 1;
+        const int yl = mc / TAX, xl = mc - yl * TAX;
+        const unsigned char* pp = patch + (yl * PX + xl) * 32;
+        u4 xv[5];
+#pragma unroll
+        for (int ks = 0; ks < 5; ++ks) xv[ks] = *reinterpret_cast<const u4*>(pp + toff[ks]);
+        const int ay = ay0 + yl, ax = ax0 + xl;
+        const uint32_t keep = (m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA) ? ~0u : 0u;
+        f4 acc[4];
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) acc[nt] = ba_l[nt];
+#pragma unroll
+        for (int ks = 0; ks < 5; ++ks)
+#pragma unroll
+          for (int nt = 0; nt < 4; ++nt)
+            acc[nt] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wa[ks][nt]),
+                                                             __builtin_bit_cast(h8, xv[ks]), acc[nt], 0, 0, 0);
+#pragma unroll
+        for (int nt = 0; nt < 4; ++nt) {
+          float v[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            if constexpr (ACT_A == 1) v[e] = acc[nt][e] * __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[nt][e]));
+            else v[e] = act_t<ACT_A>(acc[nt][e]);
+          }
+          typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+          typedef uint32_t u2 __attribute__((ext_vector_type(2)));
+          const u2 o = {__builtin_bit_cast(uint32_t, h2{(_Float16)v[0], (_Float16)v[1]}) & keep,
+                        __builtin_bit_cast(uint32_t, h2{(_Float16)v[2], (_Float16)v[3]}) & keep};
+          *reinterpret_cast<u2*>(abuf + m * APITCH + (nt * 16 + g * 4) * 2) = o;
+        }
+      }
+    };
+    unsigned char* P0 = smem;
+    unsigned char* P1 = smem + PATCH;
+    unsigned char* A0 = smem + 2 * PATCH;
+    unsigned char* A1 = A0 + ABUF;
+    // prologue: patches of tiles 0 and 1, loads of tile 2, conv A of tile 0
+    if (nmine > 0) { prefetch(tile_of(0)); commit(P0); }
+    if (nmine > 1) { prefetch(tile_of(1)); commit(P1); }
+    if (nmine > 2) prefetch(tile_of(2));
+    __syncthreads();
+    if (nmine > 0) conv_a(tile_of(0), P0, A0);
+    __syncthreads();
+    for (int i = 0; i < nmine; ++i) {
+      // phase i: the B waves run conv B of tile i from A[i % 2]; here conv A of tile i + 1
+      if (i + 1 < nmine) conv_a(tile_of(i + 1), (i & 1) ? P0 : P1, (i & 1) ? A0 : A1);
+      if (i + 2 < nmine) commit((i & 1) ? P1 : P0);   // P[i % 2]: tile i's patch, read in phase i - 1
+      if (i + 3 < nmine) prefetch(tile_of(i + 3));
+      __syncthreads();
+    }
+  } else {
+    // ---------------- B waves: conv B + epilogue ----------------
+    const int w = wave - 4;
+    u4 wfr[18][2];   // k = tap * 64 + ci: 2 n-tiles x 18 K steps
+#pragma unroll
+    for (int kk = 0; kk < 18; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        wfr[kk][j] = *reinterpret_cast<const u4*>(reinterpret_cast<const _Float16*>(p.wb) +
+                                                  (size_t)(w * 32 + j * 16 + li) * p.kpad_b + kk * 32 + g * 8);
+    unsigned char* stg = smem + 2 * PATCH + 2 * ABUF + w * STG;
+    const auto yr = make_rsrc(p.y, (uint32_t)(bordered_pixels(p.B, HB, WB) * p.yc * 2));
+    __syncthreads();   // prologue: patches
+    __syncthreads();   // prologue: conv A of tile 0
+    for (int i = 0; i < nmine; ++i) {
+      const unsigned char* abuf = smem + 2 * PATCH + (i & 1) * ABUF;
+      f4 acc[4][2];
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        const f4 bv = *reinterpret_cast<const f4*>(p.bb + w * 32 + j * 16 + g * 4) * (ACT_A == 1 ? -1.4426950408889634f : 1.0f);
+#pragma unroll
+        for (int ii = 0; ii < 4; ++ii) acc[ii][j] = bv;
+      }
+      if (p.variant != 3) {
+#pragma unroll
+        for (int kk = 0; kk < 18; ++kk) {
+          const int tap = kk >> 1, r = tap / 3, s = tap - r * 3;
+          u4 xa[4];
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii)
+            xa[ii] = *reinterpret_cast<const u4*>(abuf + ((2 * ii + r) * TAX + 2 * li + s) * APITCH + (kk & 1) * 64 + g * 16);
+#pragma unroll
+          for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+              acc[ii][j] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wfr[kk][j]),
+                                                                  __builtin_bit_cast(h8, xa[ii]), acc[ii][j], 0, 0, 0);
+        }
+      }
+      // epilogue: this wave's 32 channels of the 64 pixels -> its staging rows -> 16-byte stores
+#pragma unroll
+      for (int ii = 0; ii < 4; ++ii)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) {
+          typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+          h4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {   // acc = -log2(e) x_B under the folded SiLU
+            if constexpr (ACT_A == 1 && ACT_B == 1)
+              o[e] = (_Float16)((acc[ii][j][e] * -0.6931471805599453f) *
+                                __builtin_amdgcn_rcpf(1.0f + __builtin_amdgcn_exp2f(acc[ii][j][e])));
+            else
+              o[e] = (_Float16)act_t<ACT_B>(ACT_A == 1 ? acc[ii][j][e] * -0.6931471805599453f : acc[ii][j][e]);
+          }
+          *reinterpret_cast<h4*>(stg + (ii * 16 + li) * SPITCH + (j * 16 + g * 4) * 2) = o;
+        }
+      __builtin_amdgcn_wave_barrier();
+      int tb, oy0, ox0;
+      tile_geom(tile_of(i), tb, oy0, ox0);
+      const uint32_t tile_off = (uint32_t)(pix_index(tb, oy0, ox0, HB, WB) * p.yc * 2);
+      const uint32_t row = (uint32_t)((WB + 2 * BORDER) * p.yc * 2);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {   // chunk c = lane + 64 k: pixel c / 4 (row k), 16-byte quarter c % 4
+        const int c = lane + 64 * k, mb = c >> 2, q = c & 3;
+        const int tx = mb & 15;
+        const bool in = oy0 + k < HB && ox0 + tx < WB && p.variant != 4;
+        const uint32_t off = tile_off + k * row + (uint32_t)((tx * p.yc + p.yoff + w * 32 + q * 8) * 2);
+        __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u4*>(stg + mb * SPITCH + q * 16), yr,
+                                               in ? off : 0x80000000u, 0, 0);
+      }
+      __syncthreads();
+    }
+  }
+}
+
+template <typename S, int ACT_A, int ACT_B>
+hipError_t stem_reorg_t(const StemParams& p, hipStream_t st) {
+  const int HB = p.H / 4, WB = p.W / 4;
+  const int ntiles = p.B * ((HB + 3) / 4) * ((WB + 15) / 16);
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) !=
+                                                 hipSuccess || v <= 0)
+      v = 256;
+    return v;
+  }();
+  const int nblk = ntiles < cus ? ntiles : cus;
+  YV7_LAUNCH((stem_reorg_kernel<S, ACT_A, ACT_B>), dim3(nblk), dim3(NT_RG), 0, st, p);
+  return hipGetLastError();
+}
+
+template <typename S>
+hipError_t stem_reorg_acts(const StemParams& p, hipStream_t st) {
+  if (p.act_a == 1 && p.act_b == 1) return stem_reorg_t<S, 1, 1>(p, st);
+  if (p.act_a == 2 && p.act_b == 2) return stem_reorg_t<S, 2, 2>(p, st);
+  if (p.act_a == 0 && p.act_b == 0) return stem_reorg_t<S, 0, 0>(p, st);
+  return hipErrorInvalidValue;
+}
+
 template <typename S, int CA, int CB, int SA, int ACT_A, int ACT_B>
 hipError_t stem_t(const StemParams& p, hipStream_t st) {
   constexpr int TBY = 8, TBX = 16;
@@ -625,10 +938,14 @@ hipError_t stem_acts(const StemParams& p, hipStream_t st) {
 }  // namespace
 
 bool stem_supported(int cin, int ca, int cb, int sa) {
-  return cin == 3 && ca == 32 && cb == 64 && (sa == 1 || sa == 2);
+  return (cin == 3 && ca == 32 && cb == 64 && (sa == 1 || sa == 2)) || (cin == 12 && ca == 64 && cb == 128 && sa == 1);
 }
 
 hipError_t launch_stem(const StemParams& p, int x_dtype, hipStream_t st) {
+  if (p.reorg) {
+    if (p.H % 4 || p.W % 4) return hipErrorInvalidValue;
+    return x_dtype == 1 ? stem_reorg_acts<_Float16>(p, st) : stem_reorg_acts<float>(p, st);
+  }
   if (p.sa == 1)
     return x_dtype == 1 ? stem_acts<_Float16, 32, 64, 1>(p, st) : stem_acts<float, 32, 64, 1>(p, st);
   return x_dtype == 1 ? stem_acts<_Float16, 32, 64, 2>(p, st) : stem_acts<float, 32, 64, 2>(p, st);

@@ -196,6 +196,7 @@ struct StemParams {
   const float* bb;
   int B, H, W, yc, yoff, kpad_a, kpad_b, act_a, act_b, sa;
   int variant;          // 0; >0: microbenchmark hooks (scripts/stembench.hip)
+  int reorg;            // 1: the w6 front end (ReOrg + 12 -> 64 -> 128, wa k = tap*16 + ci), stem_reorg_kernel
 };
 
 // Host launchers (defined in the .hip files, called from the runtime).

@@ -9,7 +9,8 @@ kernel launch:
   nn.Upsample(x2 nearest)  -> UPSAMPLE
   Concat                   -> nothing: producers write their channel slice of the concat tensor directly;
                               an input that already lives in another concat (or is the input image) gets a COPY
-  ReOrg at layer 0         -> fused into the INPUT packing op (space-to-depth while converting NCHW -> NHWC)
+  ReOrg at layer 0         -> fused into the INPUT packing op (space-to-depth while converting NCHW -> NHWC);
+                              fp16 plans of the w6 front end: ReOrg + its two convs as one STEM op
   Detect / IDetect / IAuxDetect -> one DETECT op per level (1x1 conv + bias + sigmoid + decode -> z)
 Layers whose outputs never reach the head (IAuxDetect's auxiliary branch) are not emitted.
 
@@ -183,6 +184,27 @@ def _stem_candidate(layers, dtype):
     return True
 
 
+def _reorg_stem_candidate(layers, dtype):
+    """Layers 0-2 = ReOrg -> Conv(12->64, 3x3, s1) -> Conv(64->128, 3x3, s2), layers 0 and 1 read only by
+    their successor: the yolov7-w6 front end (cfg/deploy/yolov7-w6.yaml:14-16), fused into one fp16 op
+    (csrc/stem.hip, stem_reorg_kernel).  YV7_NO_STEM=1 disables."""
+    if dtype != L.DT_F16 or os.environ.get('YV7_NO_STEM') == '1' or len(layers) < 4:
+        return None
+    l0, l1, l2 = layers[0], layers[1], layers[2]
+    if not (isinstance(l0, ReOrg) and type(l1) is Conv and type(l2) is Conv and l1.f == -1 and l2.f == -1):
+        return None
+    c1, c2 = l1.conv, l2.conv
+    if not (c1.in_channels == 12 and c1.out_channels == 64 and c1.kernel_size[0] == 3 and c1.stride[0] == 1
+            and c1.padding[0] == 1 and c2.out_channels == 128 and c2.kernel_size[0] == 3 and c2.stride[0] == 2
+            and c2.padding[0] == 1 and c1.groups == 1 and c2.groups == 1 and _act_code(l1.act) == _act_code(l2.act)):
+        return None
+    for m in layers[3:]:
+        srcs = [m.f] if isinstance(m.f, int) else list(m.f)
+        if any((m.i + j if j < 0 else j) in (0, 1) for j in srcs):
+            return None
+    return True
+
+
 def compile_model(model, dtype: int, fp8=None) -> Graph:
     """fp8: {op index: activation scale} — those ops (fp8_candidates of the same model and dtype) are
     packed as YV7_WFMT_FP8 (e4m3 weights + scales); the op list is otherwise identical."""
@@ -243,13 +265,13 @@ def compile_model(model, dtype: int, fp8=None) -> Graph:
     if c_in != 3:
         raise NotImplementedError('the input packing op handles 3-channel images')
     in_c = 12 if reorg0 else 3
-    stem = _stem_candidate(layers, dtype) if not reorg0 else None
+    stem = _stem_candidate(layers, dtype) if not reorg0 else _reorg_stem_candidate(layers, dtype)
     if stem is None:
         t_in = g.add_tensor(_rup(in_c, V), 1 if reorg0 else 0)
         g.ops.append(dict(kind=L.OP_INPUT, src=-1, dst=t_in, k=2 if reorg0 else 1, cout=in_c))
     else:  # layers 0-1 run as one fused op straight from the image; tensor 0 is an unused placeholder
         t_in = g.add_tensor(V, g.max_shift)
-    if reorg0:
+    if reorg0 and stem is None:
         loc[0] = (t_in, 0)
 
     # ---- pass 2: concat placement (producers write straight into the concat tensor)
@@ -292,16 +314,19 @@ def compile_model(model, dtype: int, fp8=None) -> Graph:
 
     for m in layers:
         i = m.i
-        if not live[i] or (reorg0 and i == 0) or (stem is not None and i == 0):
+        # the fused front end: layers [0, last) are folded into the stem op written at layer `last`
+        last = (2 if reorg0 else 1) if stem is not None else -1
+        if not live[i] or (reorg0 and i == 0) or i < last:
             continue
-        if stem is not None and i == 1:
-            l0, l1 = layers[0], layers[1]
+        if i == last:
+            l0, l1 = layers[last - 1], layers[last]
             wa, ba = l0.fused_weight_bias()
             wb, bb = l1.fused_weight_bias()
-            wa_off, ba_off = _pack_conv(g, wa, ba, 3)
+            # reorg: conv A reads the 12-channel space-to-depth image, K = tap * 16 + ci
+            wa_off, ba_off = _pack_conv(g, wa, ba, 16 if reorg0 else 3)
             wb_off, bb_off = _pack_conv(g, wb, bb, l1.conv.in_channels)
-            td, do = out_of(1)
-            g.ops.insert(0, dict(kind=L.OP_STEM, src=-1, cin=3, cout=l0.conv.out_channels, k=3,
+            td, do = out_of(last)
+            g.ops.insert(0, dict(kind=L.OP_STEM, src=-1, cin=12 if reorg0 else 3, cout=l0.conv.out_channels, k=3,
                                  s=l0.conv.stride[0], pad=1, act=_act_code(l0.act), w_off=wa_off, b_off=ba_off,
                                  dst=td, dst_coff=do, cout2=l1.conv.out_channels, act2=_act_code(l1.act),
                                  w2_off=wb_off, b2_off=bb_off))

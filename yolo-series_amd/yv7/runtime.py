@@ -265,10 +265,12 @@ class Plan:
         for o in self.graph.ops:
             kind = o['kind']
             if kind == L.OP_STEM:
-                sa = o['s']
-                Ha, Wa = H // sa, W // sa
+                # cin 12: the w6 front end, conv A on the 2x space-to-depth image (ReOrg fused)
+                sa, cin = o['s'], o['cin']
+                r = 2 if cin == 12 else 1
+                Ha, Wa = H // r // sa, W // r // sa
                 ca, cb = o['cout'], o['cout2']
-                flops = 2.0 * B * Ha * Wa * ca * 27 + 2.0 * B * (Ha // 2) * (Wa // 2) * cb * 9 * ca
+                flops = 2.0 * B * Ha * Wa * ca * 9 * cin + 2.0 * B * (Ha // 2) * (Wa // 2) * cb * 9 * ca
                 # reference-boundary bytes of the two layers it replaces (input read, A write + read, B write)
                 by = B * 3 * H * W * x_bytes + 2 * B * Ha * Wa * ca * es + B * (Ha // 2) * (Wa // 2) * cb * es
                 out.append((kind, flops, by))
