@@ -1835,9 +1835,15 @@ bool p8_default(const ConvParams& p) {
   const bool one = p.k == 1 && p.s == 1 && p.pad == 0;
   const long t256 = (long)((p.M + 255) / 256) * ((p.cout + 255) / 256);
   // (1x1 K = 512 -> 512 @80, 1600 tiles: 167 -> 159 us in-network, profiles/r3u_tune.txt)
-  return on && !p.pool && p.cout >= 256 && p.cout <= 1024 && p.cout % 8 == 0 && t256 >= 200 &&
-         ((one && p.K >= 1024) || (one && p.K >= 512 && p.cout >= 512 && t256 >= 1600) ||
-          (p.k == 3 && p.cin >= 256 && p.cin % BKE == 0));
+  // Round 4, yolov7-w6 1280 bs 8 (profiles/r4_w6stem/tune_w6_dispatch.txt, one layer forced at a time,
+  // us): 1x1 768->768 @40 31.2 -> 28.4 and 1536->768 @40 49.9 -> 44.2 at 150 tiles; 3x3 s2 128->256
+  // @320 183.1 -> 156.1 and @160 47.0 -> 40.0 (the 128-input stride-2 layers).
+  const bool w6 = t256 >= 150 && ((one && p.K >= 768 && p.cout >= 768) ||
+                                  (p.k == 3 && p.s == 2 && p.cin == 128 && p.cout >= 256 && t256 >= 200));
+  return on && !p.pool && p.cout >= 256 && p.cout <= 1024 && p.cout % 8 == 0 &&
+         ((t256 >= 200 && ((one && p.K >= 1024) || (one && p.K >= 512 && p.cout >= 512 && t256 >= 1600) ||
+                           (p.k == 3 && p.cin >= 256 && p.cin % BKE == 0))) ||
+          w6);
 }
 
 hipError_t launch_p8(const ConvParams& p, bool one, hipStream_t st) {
@@ -1966,7 +1972,11 @@ Choice choose(const ConvParams& p, bool det) {
       if (t128 <= s4max && nk >= 36) c.S = 4;
     } else {
       if (t128 <= 400 || (p.K <= 256 && t128 <= 3200)) c.cfg = R128x128s2;
-      if (t128 <= 200 && p.cout <= 256) c.cfg = R128x64;
+      // 128 x 64 tiles under 200 tiles of 128 x 128, K split in two for K >= 2048 at <= 200 of them
+      // (yolov7-w6 1280 bs 8 @20, profiles/r4_w6stem/tune_w6_dispatch.txt, us: 1024->1024 21.0 -> 15.4,
+      // 2048->1024 33.0 -> 25.2, 1024->512 18.9 -> 13.7, 2048->512 32.6 -> 18.4 split, 512->384 12.3 -> 9.5)
+      if (t128 <= 200) c.cfg = R128x64;
+      if (t128 <= 200 && p.K >= 2048 && ring_tiles(p, R128x64) <= 200) c.S = 2;
     }
   }
   if (c.S > nk) c.S = nk;
@@ -2066,7 +2076,14 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // 3x3 stride-2 layers the 128 x 128 ring would split K for (under 256 of its tiles: yolov7's 256->256
   // s2 @40, w6's 768->1024 s2 @40): the stride-2 low-resolution form (profiles/r4lr/convbench_s2.txt:
   // 256->256 s2 @40 29.6 -> 25.4 us)
-  if (!det && variant == 0 && lr && p.k == 3 && p.s == 2 && (long)((p.M + 127) / 128) * ((p.cout + 127) / 128) <= 256 &&
+  // and the stride-2 layers of at most 12 800 output pixels but those with a round of 256 x 128 tiles
+  // and cout >= 512, which the 8-phase ring below serves better (profiles/r4_w6stem/tune_*.txt, us:
+  // w6 bs 8 512->768 s2 @80 134.6 -> 107.6, 256->384 s2 @80 39.5 -> 35.7; yolov7 bs 32 512->512 s2 @40
+  // p8n 76.8 vs 90.5 here)
+  const long t2n_s2 = (long)((p.M + 255) / 256) * ((p.cout + 127) / 128);
+  if (!det && variant == 0 && lr && p.k == 3 && p.s == 2 &&
+      ((long)((p.M + 127) / 128) * ((p.cout + 127) / 128) <= 256 ||
+       (p.M <= 12800 && !(t2n_s2 >= 150 && t2n_s2 <= 250 && p.cout >= 512))) &&
       lr_supported(p, 4))
     return launch_conv_lr(p, 4, st);
   // 3x3 stride-1 layers with 128-channel output tiles and at least one round of 16 x 16 x 128 tiles: the
