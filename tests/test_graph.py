@@ -143,3 +143,32 @@ def test_pool_fold(monkeypatch):
     x = frames(1, 64, 64)
     with torch.no_grad():
         torch.testing.assert_close(plan_interp.run(g, x), plan_interp.run(g0, x), rtol=0, atol=0)
+
+
+def test_reorg_stem_op():
+    """yolov7-w6's fp16 front end (ReOrg, cfg/deploy/yolov7-w6.yaml:14-16 layers 1-2) compiles to ONE stem
+    op for csrc/stem.hip's stem_reorg_kernel: conv A packed with K = tap * 16 + ci (ci 12-15 zero), conv B
+    with K = tap * 64 + ci, written into layer 2's tensor; and the fp16 plan, interpreted on the CPU
+    (tests/plan_interp.py), agrees with the fp32 plan (which keeps ReOrg in the INPUT op) to fp16 precision."""
+    import plan_interp
+    from helpers import frames
+    m = fresh_model('yolov7-w6')
+    g = compile_model(m, L.DT_F16)
+    st = g.ops[0]
+    assert st['kind'] == L.OP_STEM and (st['cin'], st['cout'], st['cout2'], st['s']) == (12, 64, 128, 1)
+    assert not any(o['kind'] == L.OP_INPUT for o in g.ops)
+    blob = g.weight_blob()
+    for (w_off, b_off, layer, cin_pad) in ((st['w_off'], st['b_off'], 1, 16), (st['w2_off'], st['b2_off'], 2, 64)):
+        w, b = m.model[layer].fused_weight_bias()
+        cout, cin = w.shape[:2]
+        kpad = _rup(9 * cin_pad, 64)
+        W = blob[w_off:w_off + _rup(cout, 32) * kpad * 2].view(torch.float16).float().view(-1, kpad)
+        unpacked = W[:cout, :9 * cin_pad].view(cout, 3, 3, cin_pad).permute(0, 3, 1, 2)
+        torch.testing.assert_close(unpacked[:, :cin], w.half().float(), rtol=0, atol=0)
+        assert torch.all(unpacked[:, cin:] == 0) and torch.all(W[:, 9 * cin_pad:] == 0)
+        assert torch.equal(blob[b_off:b_off + cout * 4].view(torch.float32), b)
+    x = frames(1, 128, 128)
+    with torch.no_grad():
+        want = plan_interp.run(compile_model(m, L.DT_F32), x)
+        got = plan_interp.run(g, x)
+    torch.testing.assert_close(got, want, rtol=2e-2, atol=2e-2)
