@@ -17,6 +17,7 @@
 //      holds their 9 taps of weight fragments in registers (loaded at entry, under the patch load)
 //   4. + bias + act -> LDS tile -> 16-byte NHWC stores into the destination channel slice.
 #include <cstdlib>
+#include <type_traits>
 
 #include "yv7_kernels.h"
 
@@ -435,51 +436,67 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
   // output stores likewise unconditional (a pixel past the image edge stores past the buffer: dropped)
   const auto yr = make_rsrc(p.y, (uint32_t)(bordered_pixels(p.B, HB, WB) * p.yc * 2));
   // per-thread store geometry: staging chunk -> (pixel row, column, channel byte offset)
+  // (chunk c = tid + k NT: NT is a whole number of pixel rows of chunks, so store k is the thread's
+  // pixel of row s_ty0 + k * NT / (TBX * CPR), the rest fixed: one base per thread, compile-time steps)
   constexpr int CPR = CB * 2 / 16;
   constexpr int NSTO = TBY * TBX * CPR / NT;
-  int s_ty[NSTO], s_tx[NSTO], s_mbo[NSTO];
-  uint32_t s_rel[NSTO];
-#pragma unroll
-  for (int k = 0; k < NSTO; ++k) {
-    const int c = tid + k * NT;
-    const int mb = c / CPR, ch = c - mb * CPR;
-    s_ty[k] = mb / TBX;
-    s_tx[k] = mb - s_ty[k] * TBX;
-    s_mbo[k] = mb * CPITCH + ch * 16;
-    s_rel[k] = (uint32_t)(((s_ty[k] * (WB + 2 * BORDER) + s_tx[k]) * p.yc + p.yoff + ch * 8) * 2);
-  }
+  static_assert(NT % (TBX * CPR) == 0, "whole staging rows per store round");
+  constexpr int RSTEP = NT / (TBX * CPR);
+  const int s_mb0 = tid / CPR, s_ch = tid - s_mb0 * CPR;
+  const int s_ty0 = s_mb0 / TBX, s_tx = s_mb0 - s_ty0 * TBX;
+  const int s_mbo0 = s_mb0 * CPITCH + s_ch * 16;
+  const uint32_t s_rel0 = (uint32_t)(((s_ty0 * (WB + 2 * BORDER) + s_tx) * p.yc + p.yoff + s_ch * 8) * 2);
+  const uint32_t s_rstep = (uint32_t)(RSTEP * (WB + 2 * BORDER) * p.yc * 2);
   auto store_prev = [&]() {
     if (pb < 0) return;
-    const uint32_t tile_off = (uint32_t)(pix_index(pb, poy0, pox0, HB, WB) * p.yc * 2);
+    const uint32_t tile_off = (uint32_t)(pix_index(pb, poy0, pox0, HB, WB) * p.yc * 2) + s_rel0;
 #pragma unroll
     for (int k = 0; k < NSTO; ++k) {
-      const bool in = poy0 + s_ty[k] < HB && pox0 + s_tx[k] < WB && p.variant != 4;
-      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u4*>(obuf + s_mbo[k]), yr,
-                                             in ? tile_off + s_rel[k] : 0x80000000u, 0, 0);
+      const bool in = poy0 + s_ty0 + k * RSTEP < HB && pox0 + s_tx < WB && p.variant != 4;
+      __builtin_amdgcn_raw_buffer_store_b128(*reinterpret_cast<const u4*>(obuf + s_mbo0 + k * RSTEP * TBX * CPITCH), yr,
+                                             in ? tile_off + k * s_rstep : 0x80000000u, 0, 0);
     }
   };
   // conv A of one group of three m-tiles (of 36) -> the A tile at ab
   const unsigned char* pbytes = reinterpret_cast<const unsigned char*>(patch);
   typedef uint32_t u2 __attribute__((ext_vector_type(2)));
-  auto conv_a_group = [&](int grp, unsigned char* ab, int ay0, int ax0) __attribute__((always_inline)) {
+  // this lane's A-pixel of each of its MA / 4 m-tiles (m-tile 4 k + wave, k = 3 grp + u): patch byte base,
+  // fixed across tiles — hoisted out of the tile loop, and the image-border mask computed only on border
+  // tiles (the division by TAX, the offsets and the mask were ~30 of the ~170 VALU instructions of every
+  // group of three m-tiles)
+  constexpr int NMW = MA / 4;
+  int pbase9[NMW];
+#pragma unroll
+  for (int k = 0; k < NMW; ++k) {
+    const int m = k * 4 * 16 + wave * 16 + li;
+    const int mc = m < NA ? m : NA - 1;   // rows past NA: computed, never read by conv B
+    const int yl = mc / TAX, xl = mc - yl * TAX;
+    pbase9[k] = (SA * yl * PX + SA * xl) * 8;
+  }
+  const int mlane = wave * 16 + li;
+  auto conv_a_group = [&](auto grpc, unsigned char* ab, int ay0, int ax0, bool interior) __attribute__((always_inline)) {
+    constexpr int grp = decltype(grpc)::value;
     u4 xv[3][2];
-    int mm[3];
-    uint32_t keep[3];
+    uint32_t keep[3] = {~0u, ~0u, ~0u};
 #pragma unroll
     for (int u = 0; u < 3; ++u) {
-      const int m = (grp * 3 + u) * 4 * 16 + wave * 16 + li;   // m-tile (grp*3+u)*4 + wave
-      mm[u] = m;
-      const int mc = m < NA ? m : NA - 1;
-      const int yl = mc / TAX, xl = mc - yl * TAX;
-      const int base = (SA * yl * PX + SA * xl) * 8;
+      const int base = pbase9[grp * 3 + u];
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks) {
         const u2 lo = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][0]);
         const u2 hi = *reinterpret_cast<const u2*>(pbytes + base + toff[ks][1]);
         xv[u][ks] = u4{lo[0], lo[1], hi[0], hi[1]};
       }
-      const int ay = ay0 + yl, ax = ax0 + xl;
-      keep[u] = (m < NA && (unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA) ? ~0u : 0u;
+    }
+    if (!interior) {   // tiles on the image border: zero the A pixels outside it (conv B's padding)
+#pragma unroll
+      for (int u = 0; u < 3; ++u) {
+        const int m = (grp * 3 + u) * 4 * 16 + mlane;
+        const int mc = m < NA ? m : NA - 1;
+        const int yl = mc / TAX, xl = mc - yl * TAX;
+        const int ay = ay0 + yl, ax = ax0 + xl;
+        keep[u] = ((unsigned)ay < (unsigned)HA && (unsigned)ax < (unsigned)WA) ? ~0u : 0u;
+      }
     }
     f4 acc[3][NAT];
 #pragma unroll
@@ -505,7 +522,7 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
         // zero outside the image (conv B's padding): one mask per packed pair of halves
         const u2 o = {__builtin_bit_cast(uint32_t, h2{(_Float16)v[0], (_Float16)v[1]}) & keep[u],
                       __builtin_bit_cast(uint32_t, h2{(_Float16)v[2], (_Float16)v[3]}) & keep[u]};
-        *reinterpret_cast<u2*>(ab + mm[u] * APITCH + (nt * 16 + g * 4) * 2) = o;
+        *reinterpret_cast<u2*>(ab + ((grp * 3 + u) * 4 * 16 + mlane) * APITCH + (nt * 16 + g * 4) * 2) = o;
       }
   };
   // conv B: 4 m-tiles x 2 n-tiles per wave, taps [t0, t0 + 3)
@@ -572,8 +589,11 @@ __global__ __launch_bounds__(NT, 2) void stem2_kernel(const StemParams p) {
       if (tile + G < ntiles) prefetch(tile + G);
       store_prev();
       __syncthreads();   // patch of this tile in LDS; staging of the previous one read
-#pragma unroll 1
-      for (int grp = 0; grp < MA / 12; ++grp) conv_a_group(grp, abuf0, ay0, ax0);
+      static_assert(MA == 36, "three groups of three m-tiles per wave");
+      const bool interior = ay0 >= 0 && ax0 >= 0 && ay0 + TAY <= HA && ax0 + TAX <= WA;
+      conv_a_group(std::integral_constant<int, 0>{}, abuf0, ay0, ax0, interior);
+      conv_a_group(std::integral_constant<int, 1>{}, abuf0, ay0, ax0, interior);
+      conv_a_group(std::integral_constant<int, 2>{}, abuf0, ay0, ax0, interior);
       __syncthreads();   // A tile complete
       f4 acc[4][2];
       conv_b_init(acc);
