@@ -122,3 +122,17 @@ def test_forward_fp16_map_parity(name):
           f'z vs fp32 oracle: coord rel {((zc - zr.double()).abs() / sc)[..., :4].max():.3g}, '
           f'vs half emulation {((zc - z16e.double()).abs() / sc)[..., :4].max():.3g}')
     assert m50 >= emu_map - 0.01 and m50 >= 0.95
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('name,H,W', [('yolov7', 128, 192), ('yolov7-w6', 256, 192)])
+def test_fp16_plan_fp32_input_matches_fp16_input(name, H, W):
+    """The fused stems read the image in either precision (csrc/stem.hip: stem2_kernel's fp32 single-pixel
+    loads, stem_reorg_kernel's fp32 pixel pairs); converting in the kernel must give the same fp16 patch
+    as converting on the host (round to nearest even both ways), so z is bit-identical."""
+    x = frames(2, H, W, seed=11)
+    m = fresh_model(name).to(DEV).half()
+    z16, _ = m(x.to(DEV).half())
+    z32, _ = m(x.to(DEV).float())
+    torch.cuda.synchronize()
+    assert torch.equal(z16, z32)
