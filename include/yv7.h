@@ -66,7 +66,9 @@ typedef enum {
   YV7_OP_UPSAMPLE = 3, /* nearest-neighbour x2 */
   YV7_OP_COPY = 4,     /* channel-slice copy (concat input that could not be written in place) */
   YV7_OP_DETECT = 5,   /* 1x1 conv + bias + sigmoid + grid/anchor decode -> z rows, raw logits */
-  YV7_OP_STEM = 6      /* fp16: image -> conv A (3->32, 3x3, stride s) -> conv B (32->64, 3x3, s2), A kept in LDS */
+  YV7_OP_STEM = 6      /* fp16: image -> conv A (3->32, 3x3, stride s) -> conv B (32->64, 3x3, s2), A kept in LDS;
+                          cin 12: the yolov7-w6 front end, image -> ReOrg (common.py:48-53) -> conv A (12->64,
+                          3x3, s1; weights K = tap*16 + ci) -> conv B (64->128, 3x3, s2) */
 } yv7_op_kind;
 
 /* One NHWC activation tensor of the plan: [B, H >> shift, W >> shift, channels]. Tensor 0 is the
