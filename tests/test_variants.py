@@ -26,7 +26,7 @@ from yv7 import _lib as L
 pytestmark = pytest.mark.gpu
 DEV = 'cuda:0'
 
-CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15,
+CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15, 17,
                  100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
                  201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274, 275, 276]
 DET_VARIANTS = [92, 97, 99]
@@ -62,11 +62,12 @@ def test_every_conv_variant(name, B, H, W):
 
 def test_variant_api_rejects_hooks():
     """Microbenchmark hooks (which skip work on purpose) and unchecked experiment schedules (the
-    round-2 ws64 / 8-phase scheduling experiments 17-19, 241-255) cannot be forced through the ABI."""
+    round-2 ws64 / 8-phase scheduling experiments 18-19, 241-255) cannot be forced through the ABI (17 is
+    now the 8-wave ws64 form, a kernel configuration)."""
     m = fresh_model('yolov7-tiny').to(DEV).half()
     plan = m.plan()
     conv = next(i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV)
-    for v in (12, 13, 14, 16, 17, 18, 19, 90, 91, 93, 94, 298, 160, 105, 211, 221, 233, 237, 238, 240, 241,
+    for v in (12, 13, 14, 16, 18, 19, 90, 91, 93, 94, 298, 160, 105, 211, 221, 233, 237, 238, 240, 241,
               248, 255, 259, 260, 261, 263, 277, 911):
         with pytest.raises(RuntimeError):
             plan.set_op_variant(conv, v)

@@ -17,7 +17,8 @@
 //    per-lane base plus a compile-time offset (no address arithmetic in the loop);
 //  * 4 waves (one per SIMD), each 4 output rows (64 pixels) x 64 channels: per 32-deep sub-step 4
 //    weight + 4 patch fragments feed 16 v_mfma_f32_16x16x32_f16 (weights as the A operand, so a
-//    lane's accumulator is 4 consecutive channels of one pixel);
+//    lane's accumulator is 4 consecutive channels of one pixel); since round 4 the default runs 8
+//    waves of 2 rows (two per SIMD, 256 VGPRs each instead of 450: NWV below);
 //  * software-pipelined across tiles: tile t's epilogue (bias = accumulator init, compile-time
 //    activation, fp16, v_permlane16_swap so each lane holds 8 consecutive channels, 16-byte stores
 //    into the destination channel slice — zero-copy concat) is issued between tile t+1's MFMAs;
@@ -57,22 +58,23 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint3
 // s ^ (n & 7) of that tap.  A thread's 18 chunks go as two batches of 9 loads issued before their LDS
 // writes (as a load -> write loop, hipcc waited out one L2 round trip per chunk: 18 in a row before
 // the first patch DMA of every block).
+template <int NTH = NT>
 __device__ __forceinline__ void load_weights(const ConvParams& p, unsigned char* wl, int tid) {
-  constexpr int NQ = 9 * CO * 8, IT = NQ / NT, NB = 9;
-  static_assert(NQ % NT == 0 && IT % NB == 0, "whole batches of chunks per thread");
+  constexpr int NQ = 9 * CO * 8, IT = NQ / NTH, NB = 9;
+  static_assert(NQ % NTH == 0 && IT % NB == 0, "whole batches of chunks per thread");
   const unsigned char* w = reinterpret_cast<const unsigned char*>(p.w);
 #pragma unroll
   for (int b0 = 0; b0 < IT; b0 += NB) {
     u4 v[NB];
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int q = tid + (b0 + j) * NT;
+      const int q = tid + (b0 + j) * NTH;
       const int t = q / (CO * 8), rem = q - t * CO * 8, n = rem >> 3, slot = rem & 7;
       v[j] = *reinterpret_cast<const u4*>(w + ((size_t)n * p.kpad + t * CI + (slot ^ (n & 7)) * 8) * 2);
     }
 #pragma unroll
     for (int j = 0; j < NB; ++j) {
-      const int q = tid + (b0 + j) * NT;
+      const int q = tid + (b0 + j) * NTH;
       const int t = q / (CO * 8), rem = q - t * CO * 8, n = rem >> 3, slot = rem & 7;
       *reinterpret_cast<u4*>(wl + t * WTAP + n * 128 + slot * 16) = v[j];
     }
@@ -84,8 +86,18 @@ __device__ __forceinline__ void load_weights(const ConvParams& p, unsigned char*
 // form has no runtime test between the MFMAs and the previous tile's epilogue: a branch there puts the
 // epilogue in its own basic block, which the sched_group_barrier pattern cannot interleave with the
 // MFMAs (round 3: the epilogue then ran as a VALU block between super-steps, ~20 % of the kernel).
-template <int ACT, int HOOK = 0>
-__global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p) {
+// NWV = 8 (round 4, variant 17): eight waves of 2 output rows each, two per SIMD — the 4-wave form runs
+// one wave per SIMD (450 registers), so nothing covers its own LDS / DMA waits (PMC: MFMA pipe 47 % busy,
+// 31 % of the wave's cycles waiting, profiles/r4_pmc_kernels/ws64_*); here a super-step is 24 MFMAs
+// from 12 weight + 4 patch fragments, and the other wave of the SIMD issues while one waits.
+template <int ACT, int HOOK = 0, int NWV = 4>
+__global__ __launch_bounds__(64 * NWV, 1) void conv3x3_ws64_kernel(const ConvParams p) {
+  constexpr int NTH = 64 * NWV;
+  constexpr int RPW = TS / NWV;                 // output rows per wave
+  constexpr int NX = RPW + 2;                   // patch rows a wave reads per super-step
+  constexpr int GPW_ = (PGROUPS + NWV - 1) / NWV;
+  constexpr int NPIECE = 2 * RPW;               // epilogue pieces (= 16-byte stores) per lane per tile
+  static_assert(NWV == 4 || NWV == 8, "4 or 8 waves");
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
   unsigned char* wl = smem + 2 * PBUF;
 
@@ -105,18 +117,18 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     for (int e = 0; e < 4; ++e) bias[j][e] = p.bias[j * 16 + g * 4 + e];
 
   // weights -> LDS once: tap t, out channel n, 16-byte slot s holds K chunk s ^ (n & 7) of that tap
-  load_weights(p, wl, tid);
+  load_weights<NTH>(p, wl, tid);
 
   // patch DMA: wave w moves groups w, w+4, ... (waves 1-3 repeat their last group so that every wave
   // issues GPW instructions: identical bytes to the same LDS addresses).  Lane l of group G: patch
   // pixel pp = 8G + (l >> 3), slot l & 7 = source chunk slot ^ (column & 7); its source offset is
   // relative to the tile's patch origin (scalar offset per tile).
-  uint32_t dvo[GPW];
-  int dgrp[GPW];
+  uint32_t dvo[GPW_];
+  int dgrp[GPW_];
 #pragma unroll
-  for (int k = 0; k < GPW; ++k) {
-    int G8 = wave + 4 * k;
-    if (G8 >= PGROUPS) G8 -= 4;
+  for (int k = 0; k < GPW_; ++k) {
+    int G8 = wave + NWV * k;
+    if (G8 >= PGROUPS) G8 -= NWV;
     dgrp[k] = G8;
     const int pp = 8 * G8 + (lane >> 3);
     const int py = pp / PS, px = pp - py * PS;
@@ -132,7 +144,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     unsigned char* base = smem + buf * PBUF;
     if constexpr (HOOK != 13 && HOOK != 16)
 #pragma unroll
-      for (int k = 0; k < GPW; ++k) dma16(xr, base + dgrp[k] * 1024, dvo[k], so);
+      for (int k = 0; k < GPW_; ++k) dma16(xr, base + dgrp[k] * 1024, dvo[k], so);
   };
 
   // per-lane LDS read bases (the tap loop adds compile-time offsets only)
@@ -144,14 +156,14 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     wbase[sub] = (uint32_t)(li * 128 + (((sub * 4 + g) ^ (li & 7)) * 16));
 #pragma unroll
     for (int s = 0; s < 3; ++s)
-      pbase[s][sub] = (uint32_t)((4 * wave * PS + li + s) * 128 + (((sub * 4 + g) ^ ((li + s) & 7)) * 16));
+      pbase[s][sub] = (uint32_t)((RPW * wave * PS + li + s) * 128 + (((sub * 4 + g) ^ ((li + s) & 7)) * 16));
   }
 
   // output offset of tile t's (4*wave + i, li) pixel row, channel g*4 (+ j*32 bytes per j)
   const uint32_t rowb = (uint32_t)((p.Wo + 2 * BORDER) * p.yc * 2);
   auto out_origin = [&](int t) -> uint32_t {
     const int b = t / tpi, rr = t - b * tpi, ty = rr / tx_n, tx = rr - ty * tx_n;
-    return (uint32_t)((pix_index(b, ty * TS + 4 * wave, tx * TS + li, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
+    return (uint32_t)((pix_index(b, ty * TS + RPW * wave, tx * TS + li, p.Ho, p.Wo) * p.yc + p.yoff) * 2);
   };
   // One tile = 6 super-steps (tap column s, 32-deep K half `sub`): 6 patch fragments (patch rows
   // 4*wave + 0..5) and 12 weight fragments (taps (0..2, s)) feed 48 MFMAs — each patch fragment
@@ -166,16 +178,16 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
       for (int j = 0; j < 4; ++j)
         wf[r][j] = *reinterpret_cast<const u4*>(wl + (r * 3 + sc) * WTAP + j * 16 * 128 + wbase[sub]);
   };
-  auto load_x = [&](const unsigned char* pb, int ss, u4 (&xf)[6]) __attribute__((always_inline)) {
+  auto load_x = [&](const unsigned char* pb, int ss, u4 (&xf)[NX]) __attribute__((always_inline)) {
     const int sc = ss >> 1, sub = ss & 1;
 #pragma unroll
-    for (int q = 0; q < 6; ++q) xf[q] = *reinterpret_cast<const u4*>(pb + q * PS * 128 + pbase[sc][sub]);
+    for (int q = 0; q < NX; ++q) xf[q] = *reinterpret_cast<const u4*>(pb + q * PS * 128 + pbase[sc][sub]);
   };
   // Super-step ss computes from set (ss & 1); set 0's weights (tap column 0, K half 0) are the same
   // for every tile, so the last super-step of a tile re-reads them for the next tile: at a tile's
   // start only the 6 patch fragments wait on LDS behind the barrier.
-  u4 wA[3][4], xA[6], wB[3][4], xB[6];   // set 0's weights are first read after the first barrier
-  auto tile_mfma = [&](const unsigned char* pb, f4 (&acc)[4][4], auto&& side) __attribute__((always_inline)) {
+  u4 wA[3][4], xA[NX], wB[3][4], xB[NX];   // set 0's weights are first read after the first barrier
+  auto tile_mfma = [&](const unsigned char* pb, f4 (&acc)[4][RPW], auto&& side) __attribute__((always_inline)) {
     load_x(pb, 0, xA);
     auto step = [&](auto ssc) __attribute__((always_inline)) {
       constexpr int ss = decltype(ssc)::value;
@@ -194,16 +206,16 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
-          for (int i = 0; i < 4; ++i)
+          for (int i = 0; i < RPW; ++i)
             acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wc[r][j]),
                                                                __builtin_bit_cast(h8, xc[i + r]), acc[j][i], 0, 0, 0);
       side(ssc);
-      // issue pattern of the super-step: the next set's fragment reads (18, or the 12 weight
+      // issue pattern of the super-step: the next set's fragment reads (12 + NX, or the 12 weight
       // fragments of the next tile's first set) ride between the first MFMAs (their latency hides
       // under the rest), the side work's VALU ops two per MFMA
-      constexpr int NR = ss + 1 < 6 ? 18 : 12;
+      constexpr int NR = ss + 1 < 6 ? 12 + NX : 12;
 #pragma unroll
-      for (int k = 0; k < 48; ++k) {
+      for (int k = 0; k < 12 * RPW; ++k) {
         __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);
         if (k < NR) __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);
         __builtin_amdgcn_sched_group_barrier(0x002, 2, 0);
@@ -224,7 +236,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
   // 2h+1 channels jb*16 + 8h .. +7: one 16-byte store per lane (a pixel's 32m .. 32m+31 channels are
   // 64 contiguous bytes from its four lanes).
   const uint32_t lane_ch = (uint32_t)((16 * (g & 1) + 8 * (g >> 1)) * 2);
-  auto epi_piece = [&](const f4 (&acc)[4][4], uint32_t o0, int q) {
+  auto epi_piece = [&](const f4 (&acc)[4][RPW], uint32_t o0, int q) {
     const int i = q >> 1, m = q & 1;
     typedef _Float16 h4 __attribute__((ext_vector_type(4)));
     h4 va, vb;
@@ -240,11 +252,11 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
     if constexpr (HOOK != 12)
       __builtin_amdgcn_raw_buffer_store_b128(v, yr, o0 + i * rowb + m * 64 + lane_ch, 0, 0);
   };
-  auto init_acc = [&](f4 (&acc)[4][4]) {
+  auto init_acc = [&](f4 (&acc)[4][RPW]) {
 #pragma unroll
     for (int j = 0; j < 4; ++j)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) acc[j][i] = f4{bias[j][0], bias[j][1], bias[j][2], bias[j][3]};
+      for (int i = 0; i < RPW; ++i) acc[j][i] = f4{bias[j][0], bias[j][1], bias[j][2], bias[j][3]};
   };
 
   // Pipeline, iteration of tile t (patch buffer b = iteration parity):
@@ -259,7 +271,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
   if (t >= TE) return;
   issue_patch(t, 0);
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // weight ds_writes of this wave
-  f4 accA[4][4], accB[4][4];
+  f4 accA[4][RPW], accB[4][RPW];
   uint32_t oprev = 0;
   int buf = 0;
   // first tile: no epilogue to interleave
@@ -275,7 +287,7 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
   // steady state, two tiles per trip so the accumulator sets swap roles without copies
   bool stores_out = false;   // the previous iteration issued an epilogue (NSTORE younger stores)
   while (t < TE) {
-    if (stores_out) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
+    if (stores_out) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPIECE) : "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     stores_out = true;
     if constexpr (HOOK != 16) __builtin_amdgcn_s_barrier();
@@ -285,18 +297,18 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
       constexpr int ss = decltype(ssc)::value;
       if constexpr (HOOK != 14 && HOOK != 16)
 #pragma unroll
-        for (int q = (ss * 4) / 3; q < ((ss + 1) * 4) / 3; ++q) epi_piece(accA, oprev, q);
+        for (int q = (ss * NPIECE) / 6; q < ((ss + 1) * NPIECE) / 6; ++q) epi_piece(accA, oprev, q);
     });
     oprev = out_origin(t);
     t += TS_;
     buf ^= 1;
     if (t >= TE) {
 #pragma unroll
-      for (int q = 0; q < 8; ++q) epi_piece(accB, oprev, q);
+      for (int q = 0; q < NPIECE; ++q) epi_piece(accB, oprev, q);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       return;
     }
-    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTORE) : "memory");
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NPIECE) : "memory");
     if constexpr (HOOK != 16) __builtin_amdgcn_s_barrier();
     if (t + TS_ < TE) issue_patch(t + TS_, buf ^ 1);
     init_acc(accA);
@@ -304,14 +316,14 @@ __global__ __launch_bounds__(NT, 1) void conv3x3_ws64_kernel(const ConvParams p)
       constexpr int ss = decltype(ssc)::value;
       if constexpr (HOOK != 14 && HOOK != 16)
 #pragma unroll
-        for (int q = (ss * 4) / 3; q < ((ss + 1) * 4) / 3; ++q) epi_piece(accB, oprev, q);
+        for (int q = (ss * NPIECE) / 6; q < ((ss + 1) * NPIECE) / 6; ++q) epi_piece(accB, oprev, q);
     });
     oprev = out_origin(t);
     t += TS_;
     buf ^= 1;
   }
 #pragma unroll
-  for (int q = 0; q < 8; ++q) epi_piece(accA, oprev, q);
+  for (int q = 0; q < NPIECE; ++q) epi_piece(accA, oprev, q);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -613,6 +625,17 @@ hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st) {
   // halo kernel keeps the @80 layers: 30.1 vs 32.2 / 34.1); the column-pair form stays the default.
   // YV7_WS64R=1: the ring form.
   static const int ring = [] { const char* e = getenv("YV7_WS64R"); return e ? atoi(e) : 0; }();
+  // the 8-wave form (two waves per SIMD; variant 17) is the default since round 4: in-network, one layer
+  // forced at a time (profiles/r4_ws8/, us, 4-wave -> 8-wave): yolov7 bs 32 @320 233.9 -> 218.2, the four
+  // @160 layers 65.7-68.1 -> 61.6-63.5; w6 bs 8 @320 64.3-68.8 -> 62.0-63.0.  Variant 11 / YV7_WS64_4=1:
+  // the 4-wave form.
+  static const int four = [] { const char* e = getenv("YV7_WS64_4"); return e ? atoi(e) : 0; }();   // A/B: 4-wave
+  if (p.variant == 17 || (p.variant != 11 && p.variant != 15 && !ring && !four)) {
+    if (p.act == 1) YV7_LAUNCH((conv3x3_ws64_kernel<1, 0, 8>), dim3(grid), dim3(512), 0, st, p);
+    else if (p.act == 2) YV7_LAUNCH((conv3x3_ws64_kernel<2, 0, 8>), dim3(grid), dim3(512), 0, st, p);
+    else YV7_LAUNCH((conv3x3_ws64_kernel<0, 0, 8>), dim3(grid), dim3(512), 0, st, p);
+    return hipGetLastError();
+  }
   if (p.variant == 11 || (p.variant != 15 && !ring)) {
     if (p.act == 1) YV7_LAUNCH((conv3x3_ws64_kernel<1>), dim3(grid), dim3(NT), 0, st, p);
     else if (p.act == 2) YV7_LAUNCH((conv3x3_ws64_kernel<2>), dim3(grid), dim3(NT), 0, st, p);
