@@ -24,7 +24,7 @@ ap = argparse.ArgumentParser()
 ap.add_argument('--model', default='yolov7')
 ap.add_argument('--b', type=int, default=32)
 ap.add_argument('--img', type=int, default=640)
-ap.add_argument('--variants', default='0,221,222,223')
+ap.add_argument('--variants', default='0,231,262,270')
 ap.add_argument('--rounds', type=int, default=3)
 ap.add_argument('--iters', type=int, default=4)
 ap.add_argument('--out', default='')

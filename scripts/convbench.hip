@@ -52,6 +52,8 @@ int main(int argc, char** argv) {
     {"3x3s2 256->256 @80", 32, 80, 80, 256, 256, 3, 2},
     {"3x3s2 256->256 @40", 32, 40, 40, 256, 256, 3, 2},
     {"3x3s2 512->512 @40", 32, 40, 40, 512, 512, 3, 2},
+    {"3x3s2 128->256 @320 b8", 8, 320, 320, 128, 256, 3, 2},
+    {"3x3s2 128->256 @160 b8", 8, 160, 160, 128, 256, 3, 2},
     {"3x3 128->256 @80", 32, 80, 80, 128, 256, 3, 1},
     {"3x3 256->512 @40", 32, 40, 40, 256, 512, 3, 1},
     {"3x3 512->1024 @20", 32, 20, 20, 512, 1024, 3, 1},

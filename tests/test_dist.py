@@ -272,6 +272,64 @@ def test_bench_launcher_starts_ranks():
     assert r['per_rank_world_size_seen'] == [2, 2] and len(r['allgather_us_per_batch']) == 2
 
 
+def test_bench_plumbing_8rank_global_batch_256():
+    """BASELINE configs[2] on CPU: `bench.py --gpus 8 --plumbing` — 8 gloo ranks of
+    yolov7, 32 images each (global batch 256): every rank receives rank 0's weight blob, the shards are the
+    contiguous eighths of the global batch, and the all-gathered detections hold all 256 images in global
+    order on every rank."""
+    import json
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ('WORLD_SIZE', 'RANK', 'LOCAL_RANK', 'MASTER_PORT')}
+    env['OMP_NUM_THREADS'] = '1'
+    out = subprocess.run([sys.executable, os.path.join(root, 'bench.py'), '--gpus', '8', '--plumbing',
+                          '--model', 'yolov7', '--batch', '32'], capture_output=True, text=True, env=env,
+                         timeout=900)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith('{')]
+    assert len(lines) == 1, out.stdout
+    r = lines[0]
+    assert r['n_gpus'] == 8 and r['rccl_world_size'] == 8 and r['world_size_seen'] == 8
+    assert r['global_batch'] == 256 and r['model'] == 'yolov7'
+    assert r['shards'] == [[32 * k, 32 * k + 32] for k in range(8)]
+    assert r['gathered_in_global_order'] == [True] * 8 and r['all_ranks_ok']
+    assert r['per_rank_world_size_seen'] == [8] * 8 and len(r['allgather_us_per_batch']) == 8
+
+
+def test_gloo_world2_fp8_scales_missing_on_rank0():
+    """A scale missing from rank 0's dict fails on EVERY rank after the broadcast (rank 0 used
+    to raise alone and leave the others waiting in the collective)."""
+    ctx = mp.get_context('spawn')
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_fp8_missing_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=300) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    assert res == [(0, 'KeyError'), (1, 'KeyError')]
+
+
+def _fp8_missing_worker(rank, world, port, q):
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path[:0] = [os.path.join(root, 'yolo-series_amd'), root]
+    os.environ.update(MASTER_ADDR='127.0.0.1', MASTER_PORT=str(port))
+    dist.init_process_group('gloo', rank=rank, world_size=world)
+    try:
+        from yv7.dist import broadcast_fp8_scales
+        scales = {3: 0.5, 7: 0.25} if rank == 0 else None   # op 9 has no scale on rank 0
+        try:
+            broadcast_fp8_scales(scales, [3, 7, 9], torch.device('cpu'))
+            q.put((rank, 'ok'))
+        except KeyError:
+            q.put((rank, 'KeyError'))
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.mark.gpu
 def test_rccl_world1_broadcast_gather_inflight():
     """The RCCL data path on one MI355X (world size 1, the collectives issued anyway): the weight blob

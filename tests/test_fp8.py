@@ -156,33 +156,36 @@ def test_gpu_fp8_fused_quantize_matches_staged(name, B, H, W):
 @pytest.mark.parametrize('name', ['yolov7', 'yolov7-tiny'])
 def test_gpu_fp8_map_parity(name):
     """configs[4] parity: mAP@0.5 of the GPU fp8 plan's detections against the oracle's fp32 detections
-    (the metric's ground truth) and against the oracle's restatement of the fp8 arithmetic on the same
-    scales (fp16 storage elsewhere); conf 0.25 / iou 0.45, 2 frames at 640."""
-    x = frames(2, 640, 640, seed=8)
+    (the metric's ground truth), next to the oracle's restatement of the fp8 arithmetic on the same scales
+    (fp16 storage elsewhere) scored the same way; conf 0.25 / iou 0.45, 32 frames at 640 in ONE batch of
+    32 (the bench's fp8 dispatch).
+
+    Why 32 frames: e4m3 rounding is chaotic — an fp16 input one ulp away rounds to
+    the neighbouring e4m3 value — so the GPU plan and the restatement agree with each other only at mAP
+    ~0.6-0.85, and on 2 frames their scores against the fp32 oracle differed by up to 0.04 either way
+    (round 4: 0.539 vs 0.560 for yolov7).  Over 32 frames that per-frame chaos averages out, so the
+    round-3 bar is back: the GPU plan may trail the restatement of its own arithmetic by at most 0.02.
+    The absolute floors only catch a collapse (they are not fitted: e4m3 on both operands costs this
+    random-weight network about half its detections)."""
+    NF = 32
+    x = frames(NF, 640, 640, seed=8)
     plan = _gpu_fp8_plan(name, None)
     z, _ = plan.forward(x.cuda().half(), want_raw=False)
     pred = [d.cpu() for d in nms_ref.non_max_suppression(z.cpu(), 0.25, 0.45)]
     net, fused = oracle_net(name)
+    f8 = yolo_ref.fp8_fused(fused, _entries(plan.graph))
     with torch.no_grad():
-        zr, _ = yolo_ref.forward(net, fused, x)
-        ze, _ = yolo_ref.forward(net, yolo_ref.fp8_fused(fused, _entries(plan.graph)), x, half_storage=True)
+        zr = torch.cat([yolo_ref.forward(net, fused, x[i:i + 4])[0] for i in range(0, NF, 4)])
+        ze = torch.cat([yolo_ref.forward(net, f8, x[i:i + 4], half_storage=True)[0] for i in range(0, NF, 4)])
     gt = [metrics_ref.dets_as_labels(d) for d in nms_ref.non_max_suppression(zr, 0.25, 0.45)]
     ge = [metrics_ref.dets_as_labels(d) for d in nms_ref.non_max_suppression(ze, 0.25, 0.45)]
     m32, _ = metrics_ref.map_from_lists(pred, gt)
     memu, _ = metrics_ref.map_from_lists(pred, ge)
     emu32, _ = metrics_ref.map_from_lists([d for d in nms_ref.non_max_suppression(ze, 0.25, 0.45)], gt)
-    print(f'\n{name} fp8: mAP@0.5 vs fp32 oracle {m32:.4f} (oracle fp8 restatement vs fp32: {emu32:.4f}), '
-          f'vs fp8 restatement {memu:.4f}; dets {[len(d) for d in pred]}')
-    # e4m3 costs this random-weight network a large share of its detections (the restatement loses as
-    # much as the kernels do), and the loss is chaotic: an fp16 input one ulp away rounds to another e4m3
-    # value, so the GPU plan and the restatement of its arithmetic agree with each other only at mAP
-    # ~0.6-0.85, and each scores within a few hundredths of the other against the fp32 oracle.  Measured
-    # on MI355X (yolov7 / yolov7-tiny vs the fp32 oracle): round 3 0.588 / 0.668; round 4, after the
-    # fp16 3x3 layers moved to conv_lr.hip's summation order, 0.539 / 0.670 with the restatement at
-    # 0.560 / 0.649.  The config is frozen as a measured cost (DESIGN §4.4, VERDICT r3 item 6): no worse
-    # than the restatement by more than that noise, and an absolute floor (fp16 plans: >= 0.97).
-    assert m32 >= emu32 - 0.04
-    assert m32 >= {'yolov7': 0.5, 'yolov7-tiny': 0.55}[name]
+    print(f'\n{name} fp8 ({NF} frames): mAP@0.5 vs fp32 oracle {m32:.4f} (oracle fp8 restatement vs fp32: '
+          f'{emu32:.4f}), vs fp8 restatement {memu:.4f}; dets/frame {sum(len(d) for d in pred) / NF:.1f}')
+    assert m32 >= emu32 - 0.02
+    assert m32 >= {'yolov7': 0.4, 'yolov7-tiny': 0.45}[name]
 
 
 @pytest.mark.gpu

@@ -10,7 +10,8 @@ splits (1CS: configuration C, S splits; the split-K hand-off of splitk_reduce), 
 (201-206), the 8-phase rings (231: 256 x 256, 232: 256 x 128), the weight-stationary 1x1 rings (234-236,
 and 239: N-split), the column-group 3x3 halo ring (262), the
 low-resolution 3x3 kernel (270-273: 80 / 64-pixel tiles of 4 images x 4 columns, 128 / 64 channels;
-274: stride 2; 275 / 276: 160-pixel tiles) and
+274: stride 2; 275 / 276: 160-pixel tiles), the register-weight stride-2 kernel (280-284: cin 64 / 128,
+4 or 3 ring slots, 4 / 8-row tiles) and
 the alternative Detect heads (92, 97, and 99: the 64 x 256 ring that was the default before the
 persistent head).  A variant a layer's shape
 does not support falls back to the tuned kernel, which the check then covers again.
@@ -28,7 +29,8 @@ DEV = 'cuda:0'
 
 CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15, 17,
                  100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
-                 201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274, 275, 276]
+                 201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274, 275, 276,
+                 280, 281, 282, 283, 284]
 DET_VARIANTS = [92, 97, 99]
 
 
@@ -56,6 +58,55 @@ def test_every_conv_variant(name, B, H, W):
         out = check_ops(plan, x, B, H, W, raw=xs, z=z)
         lines.append(f'variant {v}: ' + kernel_summary(out))
         for i in (dets if v in DET_VARIANTS else convs):
+            plan.set_op_variant(i, 0)
+    print('\n' + '\n'.join(lines))
+
+
+# A net with the shapes the fragment kernels mask: 3x3 layers with cout % 32 == 16 (cout = 80:
+# the permlane16 pair store of the 32-channel pair 64..95 is half masked), stride-2 layers with cin 64
+# and 128 (conv_s2.hip's two weight layouts), and batches with a partial trailing 4-image group after
+# full ones (B = 5, 6).
+RAGGED = {'nc': 3, 'depth_multiple': 1.0, 'width_multiple': 1.0,
+          'anchors': [[10, 13, 16, 30, 33, 23], [30, 61, 62, 45, 59, 119], [116, 90, 156, 198, 373, 326]],
+          'backbone': [[-1, 1, 'Conv', [32, 3, 1]],    # 0  @1
+                       [-1, 1, 'Conv', [64, 3, 2]],    # 1  @2
+                       [-1, 1, 'Conv', [80, 3, 1]],    # 2  lr, cin 64 -> 80
+                       [-1, 1, 'Conv', [64, 1, 1]],    # 3
+                       [-1, 1, 'Conv', [80, 3, 2]],    # 4  @4: s2, cin 64 -> 80
+                       [-1, 1, 'Conv', [128, 1, 1]],   # 5
+                       [-1, 1, 'Conv', [80, 3, 2]],    # 6  @8: s2, cin 128 -> 80
+                       [-1, 1, 'Conv', [128, 1, 1]],   # 7
+                       [-1, 1, 'Conv', [80, 3, 1]],    # 8  lr, cin 128 -> 80 (P3)
+                       [-1, 1, 'Conv', [64, 1, 1]],    # 9
+                       [-1, 1, 'Conv', [80, 3, 2]],    # 10 @16: s2, cin 64 (P4)
+                       [-1, 1, 'Conv', [128, 1, 1]],   # 11
+                       [-1, 1, 'Conv', [96, 3, 2]]],   # 12 @32: s2, cin 128 (P5)
+          'head': [[[8, 10, 12], 1, 'Detect', ['nc', 'anchors']]]}
+
+
+@pytest.mark.parametrize('B', [5, 6])
+def test_fragment_kernels_ragged(B):
+    """The fragment kernels (conv_lr.hip 270-276, conv_s2.hip 280-284) on partial trailing image groups
+    and half-masked channel pairs, op by op against fp32 torch."""
+    import copy
+    from models.yolo import Model
+    from yv7.synthetic import synthetic_state_dict
+    m = Model(copy.deepcopy(RAGGED))
+    m.load_state_dict(synthetic_state_dict(m, seed=3, calib_hw=256))
+    m = m.float().eval().fuse().to(DEV).half()
+    plan = m.plan()
+    H = W = 256
+    x = frames(B, H, W, seed=7).to(DEV).half()
+    convs = [i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV]
+    lines = []
+    for v in [0, 270, 271, 272, 273, 274, 275, 276, 280, 281, 282, 283, 284]:
+        for i in convs:
+            plan.set_op_variant(i, v)
+        z, xs = plan.forward(x)
+        torch.cuda.synchronize()
+        out = check_ops(plan, x, B, H, W, raw=xs, z=z)
+        lines.append(f'variant {v}: ' + kernel_summary(out))
+        for i in convs:
             plan.set_op_variant(i, 0)
     print('\n' + '\n'.join(lines))
 

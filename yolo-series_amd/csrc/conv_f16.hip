@@ -2045,6 +2045,11 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     return launch_conv_hring(p, device_cus(), st);
   // the low-resolution 3x3 kernel (conv_lr.hip): 270 + tile configuration
   if (!det && variant >= 270 && variant <= 276 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
+  // the register-weight stride-2 kernel (conv_s2.hip): 280 + tile configuration
+  if (!det && variant >= 280 && variant <= 284 && s2_supported(p, variant - 280))
+    return launch_conv_s2(p, variant - 280, device_cus(), st);
+  if (!det && variant >= 285 && variant <= 289 && s2_supported(p, variant <= 287 ? 0 : 2))   // its hooks (convbench)
+    return launch_conv_s2(p, variant <= 287 ? 0 : 2, device_cus(), st);
   // 3x3 stride-1 layers of up to 204 800 output pixels (yolov7 640 bs 32 from 80^2 down, yolov7-w6 1280
   // bs 8 from 160^2 down): the low-resolution kernel (conv_lr.hip) — one layer forced at a time in the bs-32
   // forward (profiles/r4lr/tune3.txt, us, dispatch -> lr): 3x3 256->256 @20 32.2 -> 22.1, 512->512 @20

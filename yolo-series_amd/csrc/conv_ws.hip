@@ -622,8 +622,8 @@ hipError_t launch_conv_ws64(const ConvParams& p, hipStream_t st) {
   }
   // the two forms measured equal in-network (scripts/tune_ops.py, one layer forced at a time, same box,
   // us, 11 / 15: @320 228.2 / 228.4, @160 73.7 / 71.6, 71.4 / 69.8, 71.4 / 70.8, 72.3 / 71.1 — and the
-  // halo kernel keeps the @80 layers: 30.1 vs 32.2 / 34.1); the column-pair form stays the default.
-  // YV7_WS64R=1: the ring form.
+  // halo kernel keeps the @80 layers: 30.1 vs 32.2 / 34.1); of those two 4-wave forms the column-pair one
+  // is the 4-wave choice, but the default is now the 8-wave form below.  YV7_WS64R=1: the ring form.
   static const int ring = [] { const char* e = getenv("YV7_WS64R"); return e ? atoi(e) : 0; }();
   // the 8-wave form (two waves per SIMD; variant 17) is the default since round 4: in-network, one layer
   // forced at a time (profiles/r4_ws8/, us, 4-wave -> 8-wave): yolov7 bs 32 @320 233.9 -> 218.2, the four

@@ -113,10 +113,18 @@ int kpad_of(const yv7_op_desc& o) {
   return (o.k * o.k * o.cin + 63) / 64 * 64;
 }
 bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7_WFMT_FP8; }
-// 3x3 / stride-1 or 2 / pad-1 fp16 convs get a fragment-packed weight copy (conv_lr.hip)
+// 3x3 / stride-1 or 2 / pad-1 fp16 convs of a shape the fragment kernels accept (conv_lr.hip lr_supported:
+// cin / 32 in {2, 4, 6, 8, 12, 16, 24}, cout % 16 == 0, cout <= 1024; conv_s2.hip: cin 64 / 128) get a
+// fragment-packed weight copy — none at all with YV7_LR=0 (the fragment kernels then never run: the
+// forced variants 270-276 / 280-284 fall back to the tuned kernel).  yolov7: 36.9 MB, yolov7-w6: 60.5 MB
+// per fp16 plan.
 bool wants_frag(int dtype, const yv7_op_desc& o) {
-  return dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && o.k == 3 && (o.s == 1 || o.s == 2) &&
-         o.pad == 1 && !o.pool && o.cin % 32 == 0;
+  static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
+  const int nch = o.cin / 32;
+  return lr && dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && o.k == 3 && (o.s == 1 || o.s == 2) &&
+         o.pad == 1 && !o.pool && o.cin % 32 == 0 &&
+         (nch == 2 || nch == 4 || nch == 6 || nch == 8 || nch == 12 || nch == 16 || nch == 24) && o.cout % 16 == 0 &&
+         o.cout <= 1024;
 }
 
 // Geometry / operand fields of a CONV or DETECT op's kernel parameters (pointers into the workspace
@@ -303,13 +311,19 @@ int yv7_plan_create(const yv7_net_desc* d, const void* weights, size_t nbytes, i
       wf_total = align256(wf_total + yv7::frag_bytes(p->ops[i].cin, p->ops[i].cout, p->ops[i].k * p->ops[i].k));
     }
   if (wf_total) {
+    // packed on a private stream and waited for on that stream only (a device-wide sync here
+    // made plan creation wait for other plans' forwards on their own streams).  A blocking stream: its
+    // work is ordered after the null stream's weight copy above.
+    hipStream_t ps = nullptr;
     e = hipMalloc(&p->wfrag, wf_total);
+    if (e == hipSuccess) e = hipStreamCreate(&ps);
     for (size_t i = 0; e == hipSuccess && i < p->ops.size(); ++i)
       if (p->wf_off[i] >= 0)
         e = yv7::pack_frag(reinterpret_cast<const unsigned char*>(p->weights) + p->ops[i].w_off, kpad_of(p->ops[i]),
                            p->ops[i].cin, p->ops[i].cout, p->ops[i].k * p->ops[i].k,
-                           reinterpret_cast<unsigned char*>(p->wfrag) + p->wf_off[i], nullptr);
-    if (e == hipSuccess) e = hipDeviceSynchronize();
+                           reinterpret_cast<unsigned char*>(p->wfrag) + p->wf_off[i], ps);
+    if (e == hipSuccess) e = hipStreamSynchronize(ps);
+    if (ps) (void)hipStreamDestroy(ps);
     if (e != hipSuccess) {
       yv7_plan_destroy(p);
       return hip_fail(e, "yv7_plan_create: fragment packing");
@@ -401,7 +415,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15 || v == 17) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
   return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
-         (v >= 270 && v <= 276);
+         (v >= 270 && v <= 276) || (v >= 280 && v <= 284);
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {

@@ -50,21 +50,28 @@ def broadcast_weights(model, device, dtype, group=None):
 
 def broadcast_fp8_scales(scales, ops, device, group=None):
     """Rank 0's {op: activation scale} for the fp8 ops `ops` (the same list on every rank: it comes from
-    the host-side graph) -> the same dict on every rank, by one broadcast."""
+    the host-side graph) -> the same dict on every rank, by one broadcast.  A scale missing on rank 0
+    travels as NaN, so every rank raises together after the collective (a KeyError on rank 0
+    alone left the other ranks waiting in the broadcast)."""
     if dist.get_rank(group) == 0:
-        t = torch.tensor([float(scales[i]) for i in ops], dtype=torch.float64, device=device)
+        t = torch.tensor([float(scales[i]) if scales is not None and i in scales else float('nan') for i in ops],
+                         dtype=torch.float64, device=device)
     else:
         t = torch.zeros(len(ops), dtype=torch.float64, device=device)
     if len(ops):
         dist.broadcast(t, src=0, group=group)
-    return {i: float(v) for i, v in zip(ops, t.tolist())}
+    vals = t.tolist()
+    missing = [i for i, v in zip(ops, vals) if v != v]
+    if missing:
+        raise KeyError(f'broadcast_fp8_scales: rank 0 has no activation scale for fp8 ops {missing}')
+    return {i: float(v) for i, v in zip(ops, vals)}
 
 
 def broadcast_fp8_plan(model, device, min_cout=None, calib=None, group=None, scales=None):
     """BASELINE configs[4] on N ranks: rank 0 calibrates (Plan.fp8_scales) — or takes `scales` — every
     rank receives the scales, compiles the fp8 graph with them, and gets rank 0's packed blob, as
-    broadcast_weights does for the fp16 plan.  Returns (plan, graph); plan is None on a CPU device (the
-    --plumbing check)."""
+    broadcast_weights does for the fp16 plan.  Returns (plan, graph, blob): the Plan (None on a CPU
+    device: the --plumbing check), the compiled fp8 graph and rank 0's packed weight blob."""
     from yv7.graph import FP8_MIN_COUT, fp8_candidates
     min_cout = FP8_MIN_COUT if min_cout is None else min_cout
     ops = fp8_candidates(compile_model(model, L.DT_F16), min_cout)
