@@ -138,6 +138,7 @@ int main(int argc, char** argv) {
     for (int v : variants) {
       p.variant = v;
       p.y = v == 0 ? (void*)y0 : (void*)y;
+      CK(hipMemset(p.y, 0, ny * 2));   // (a hook variant's garbage must not reach the next shape's border)
       if (yv7::launch_conv(1, p, false, 0) != hipSuccess) { (void)hipGetLastError(); printf(" |%d -", v); continue; }
       for (int i = 0; i < 2; ++i) CK(yv7::launch_conv(1, p, false, 0));
       CK(hipDeviceSynchronize());

@@ -2078,6 +2078,17 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     }
     if (lr_supported(p, cfg)) return launch_conv_lr(p, cfg, st);
   }
+  // 3x3 stride-2 layers with 64 / 128 input channels and at least 204 800 output pixels: the register-weight
+  // stride-2 kernel (conv_s2.hip).  In-network, one layer forced at a time (scripts/tune_ops.py,
+  // profiles/r5_s2/tune_*.txt, us, dispatch -> s2): yolov7 bs 32 64->128 s2 @320 186.1 -> 130.4 (cfg 0),
+  // 128->128 s2 @160 102.2 -> 74.0 (cfg 3); yolov7-w6 bs 8 128->256 s2 @320 159.2 -> 123.6 (cfg 4).  The
+  // 51 200-pixel layers (128->128 s2 @80, w6 128->256 s2 @160) are equal either way and keep the
+  // dispatch below.  YV7_S2=0: off.
+  static const int s2k = [] { const char* e = getenv("YV7_S2"); return e ? atoi(e) : 1; }();
+  if (!det && variant == 0 && s2k && p.k == 3 && p.s == 2 && (long)p.M >= 204800 && (p.cin == 64 || p.cin == 128)) {
+    const int cfg = p.cin == 64 ? 0 : (p.cout >= 256 ? 4 : 3);
+    if (s2_supported(p, cfg)) return launch_conv_s2(p, cfg, device_cus(), st);
+  }
   // 3x3 stride-2 layers the 128 x 128 ring would split K for (under 256 of its tiles: yolov7's 256->256
   // s2 @40, w6's 768->1024 s2 @40): the stride-2 low-resolution form (profiles/r4lr/convbench_s2.txt:
   // 256->256 s2 @40 29.6 -> 25.4 us)

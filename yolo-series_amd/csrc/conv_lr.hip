@@ -51,7 +51,7 @@ template <int S> __host__ __device__ constexpr int col_slot(int c) { return S ==
 // 2*wm*TM .. 2*wm*TM + 2*TM once per column step, output row i taking rows 2i + r).  Images past B
 // (B not a multiple of 4) read zeros (past the input's buffer range) and store nothing.
 template <int WM, int WN, int TN, int TM, int NCH, int ACT, int PD, int S>
-__global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) : 1) void conv3x3_lr_kernel(const ConvParams p) {
+__global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) : 1) void conv3x3_lr_kernel(const ConvParams p, int ngx) {
   constexpr int NT = 64 * WM * WN;
   constexpr int TH = TM * WM, PR = S * TH + 3 - S, PC = patch_cols<S>();
   constexpr int NXA = S * TM + 3 - S;            // patch rows a wave reads per column step
@@ -68,14 +68,24 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, li = lane & 15;
 
-  // tile: XCD-major (blockIdx % 8 is the XCD on the round-robin dispatch): XCD x takes the contiguous
-  // eighth of the tiles, neighbours share patch halos and (over the n tiles) the same pixels
-  const int G = gridDim.x, bid = blockIdx.x;
-  int t = (G % 8 == 0) ? (bid % 8) * (G / 8) + bid / 8 : bid;
+  // tile: XCD-aware (blockIdx % 8 is the XCD on the round-robin dispatch).  The 8 XCDs form ngx N groups
+  // x 8 / ngx pixel groups: XCD x holds N slices (x % ngx) * nN / ngx .. + nN / ngx (its share of the
+  // weights stays in its 4 MiB L2: ngx is chosen so that share is <= 2.5 MiB) and the (x / ngx)-th
+  // contiguous range of pixel tiles (neighbours share patch halos).  ngx = 1: every XCD streams all
+  // slices over its eighth of the pixels (the 4.7-9.4 MB weights of the 512-input
+  // layers re-fetched from MALL/HBM per tile on every XCD, 5.3x the algorithmic bytes).
+  const int bid = blockIdx.x;
   const int nN = (p.cout + BN - 1) / BN;
-  const int nt = t % nN;
-  t /= nN;
   const int ncg = p.Wo / FC;
+  const int nrg_ = p.Ho / TH, nig = (p.B + FI - 1) / FI;
+  const int P = nig * nrg_ * ncg;               // pixel tiles
+  const int npx = 8 / ngx, nsl = nN / ngx;      // pixel groups, N slices per XCD
+  const int xcd = bid % 8, k = bid / 8;
+  const int pper = (P + npx - 1) / npx;         // pixel tiles per pixel group
+  const int pi = (xcd / ngx) * pper + k / nsl;
+  if (k / nsl >= pper || pi >= P) return;       // (the grid is 8 * nsl * pper blocks)
+  const int nt = (xcd % ngx) * nsl + k % nsl;
+  int t = pi;
   const int x0 = (t % ncg) * FC;
   t /= ncg;
   const int nrg = p.Ho / TH;   // (t / nrg: image group, ceil(B / 4) of them)
@@ -253,10 +263,24 @@ __global__ void pack_frag_kernel(const _Float16* w, int kpad, int cin, int nfrag
 template <int WM, int WN, int TN, int TM, int PD, int S, int NCH>
 hipError_t launch_cfg(const ConvParams& p, hipStream_t st) {
   constexpr int TH = TM * WM, BN = WN * TN * 16;
-  const long T = (long)((p.B + FI - 1) / FI) * (p.Ho / TH) * (p.Wo / FC) * ((p.cout + BN - 1) / BN);
-  if (p.act == 1) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 1, PD, S>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
-  else if (p.act == 2) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 2, PD, S>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
-  else YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 0, PD, S>), dim3((unsigned)T), dim3(64 * WM * WN), 0, st, p);
+  const long P = (long)((p.B + FI - 1) / FI) * (p.Ho / TH) * (p.Wo / FC);
+  const int nN = (p.cout + BN - 1) / BN;
+  // N groups over the XCDs: the fewest (a divisor of both 8 and nN) that keep one XCD's weight share
+  // under 2.5 MiB (YV7_LR_NGX forces a value for A/B runs)
+  static const int force = [] { const char* e = getenv("YV7_LR_NGX"); return e ? atoi(e) : 0; }();
+  const double wbytes = (double)p.cout * 9 * p.cin * 2;
+  int ngx = 1;
+  if (force > 0) {
+    ngx = force;
+  } else {
+    while (ngx < 8 && nN % (2 * ngx) == 0 && wbytes / ngx > 2.5 * 1048576.0) ngx *= 2;
+  }
+  if (ngx < 1 || 8 % ngx || nN % ngx) ngx = 1;
+  const int npx = 8 / ngx, nsl = nN / ngx;
+  const long grid = 8L * nsl * ((P + npx - 1) / npx);
+  if (p.act == 1) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 1, PD, S>), dim3((unsigned)grid), dim3(64 * WM * WN), 0, st, p, ngx);
+  else if (p.act == 2) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 2, PD, S>), dim3((unsigned)grid), dim3(64 * WM * WN), 0, st, p, ngx);
+  else YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 0, PD, S>), dim3((unsigned)grid), dim3(64 * WM * WN), 0, st, p, ngx);
   return hipGetLastError();
 }
 

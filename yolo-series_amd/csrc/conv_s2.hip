@@ -13,22 +13,27 @@
 //  * a block holds its N slice's whole weight matrix in VGPRs for the whole (persistent) launch: wave
 //    (ng, pg) keeps TN x 9 x NCH fragments (16 channels x 32 K each, 4 VGPRs) — 144 VGPRs for
 //    cin = 64 / TN = 2 and cin = 128 / TN = 1 — loaded ONCE from the fragment-packed copy (pack_frag);
-//  * pixels stream: per 32-channel chunk a tile's input patch is DMA'd (buffer_load ... lds) into an
-//    NS-slot LDS ring once, and every LDS read of a pixel fragment feeds up to 3 x TN MFMAs: the MFMA's 16
+//  * pixels stream: per 64-channel chunk (one full 128-byte line of every input pixel: a DMA piece is 8
+//    whole lines) a tile's input patch is DMA'd (buffer_load ... lds) into an NS-slot LDS ring once, and
+//    every LDS read of a pixel fragment feeds up to 3 x TN MFMAs: the MFMA's 16
 //    pixels are 4 IMAGES x 4 COLUMNS of one output row (conv_lr.hip's fragment), a wave owns TM output
 //    rows of one 4-column group and reads the 2 TM + 1 patch rows of a tap column once — output row i
 //    takes patch rows 2i, 2i + 1, 2i + 2 for taps r = 0, 1, 2, so input rows 2y + 1 are shared by output
 //    rows y and y + 1 (the halo-ring column-group reuse at stride 2);
 //  * the patch keeps even input columns first (slot c / 2) and odd ones after (4 PG + 1 + c / 2), so the
-//    four columns 2x + s a tap reads are four consecutive slots; 16-byte chunk q of image i sits at
-//    q ^ f(i), f = {0, 2, 3, 1} (conv_lr.hip: conflict-free ds_read_b128 for every slot offset) — the
-//    swizzle is applied on the DMA's per-lane SOURCE address, the LDS image is lane-linear;
-//  * 8 waves (two per SIMD) in two stagger groups one barrier apart (waves 4-7 behind; a SIMD hosts
-//    waves w and w + 4): a group's tile epilogue (activation, fp16, stores) issues beside the other
-//    group's MFMAs.  One barrier per chunk; the DMA of chunk k + L (L = NS - 2) is issued in the interval
-//    after barrier k into the slot chunk k - 2 left, and every wave waits only for its own pieces of
+//    four columns 2x + s a tap reads are four consecutive slots; a pixel's 128 bytes are 8 16-byte
+//    positions, K-step half h's part g at position (4 h + g) ^ 2 (slot & 3) — conflict-free ds_read_b128
+//    for every row, slot offset and half (checked exhaustively against the gfx950 lane groups,
+//    scripts/s2_swizzle_check.py); the swizzle is applied on the DMA's per-lane SOURCE address, the LDS
+//    image is lane-linear.  (The first form fetched 64-byte half lines per 32-channel chunk: the DMA path,
+//    not the MFMAs, bound it — 166 us on 64->128 @320, 62 us with the DMA hooked out.)
+//  * 8 waves (two per SIMD); one barrier per chunk; the DMA of chunk k + L is issued in the interval after
+//    barrier k into the slot the chunks before it left, and every wave waits only for its own pieces of
 //    the chunk the next interval reads (counted vmcnt: the pieces per wave and the epilogue stores per
-//    tile are compile-time constants; pieces past the patch go to the slot's padding).
+//    tile are compile-time constants; pieces past the patch go to the slot's padding).  STG = 1: two
+//    stagger groups one barrier apart (waves 4-7 behind; a SIMD hosts waves w and w + 4), so a group's
+//    tile epilogue issues beside the other group's MFMAs, at the cost of one ring slot (L = NS - 2; STG =
+//    0: L = NS - 1).
 #include "yv7_kernels.h"
 
 namespace yv7 {
@@ -36,10 +41,8 @@ namespace yv7 {
 namespace {
 
 constexpr int FI = 4, FC = 4;   // MFMA pixel fragment: 4 images x 4 columns
-constexpr int CK = 32;          // channels per chunk (one MFMA K step)
+constexpr int DC = 64;          // channels per DMA chunk (one 128-byte line per pixel; two MFMA K steps)
 constexpr uint32_t OOB = 0x80000000u;
-
-__host__ __device__ constexpr int swz(int img) { return (0x1320 >> (4 * img)) & 3; }
 
 template <int N>
 __device__ __forceinline__ void vmwait() {
@@ -51,42 +54,45 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint3
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, vo, so, 0, 0);
 }
 
-// Compile-time geometry of one configuration.
-template <int NCH, int TN, int TM, int PG, int NG, int NS>
+// position swizzle of a pixel's eight 16-byte parts by its column slot
+__host__ __device__ constexpr int pswz(int slot) { return 2 * (slot & 3); }
+
+// Compile-time geometry of one configuration.  NCH = cin / 32 (MFMA K steps per tap).
+template <int NCH, int TN, int TM, int PG, int NG, int NS, int STG>
 struct S2Geo {
   static constexpr int NW = NG * PG;                       // waves
-  static_assert(NW == 8, "two stagger groups of four waves");
+  static_assert(NW == 8, "eight waves");
+  static_assert(NCH % 2 == 0, "whole 64-channel DMA chunks");
+  static constexpr int NDC = NCH / 2;                      // DMA chunks per tile
   static constexpr int PR = 2 * TM + 1;                    // patch rows
   static constexpr int NEV = 4 * PG + 1;                   // even patch columns (slots 0 .. NEV - 1)
   static constexpr int PC = 8 * PG + 1;                    // patch columns
   static constexpr int PPX = FI * PR * PC;                 // patch pixels
-  static constexpr int NP = (PPX + 15) / 16;               // 1 KiB DMA pieces (16 pixels x 64 B)
+  static constexpr int NP = (PPX + 7) / 8;                 // 1 KiB DMA pieces (8 pixels x 128 B)
   static constexpr int PW = (NP + NW - 1) / NW;            // pieces per wave per chunk
   static constexpr int SB = NW * PW * 1024;                // bytes per ring slot (padded to whole pieces)
   static constexpr int LDS = NS * SB;
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  static constexpr int L = NS - 2;                         // DMA lead in chunks
+  static constexpr int L = NS - 1 - STG;                   // DMA lead in chunks
   static_assert(L >= 1 && L <= 2, "lead");
   static constexpr int BN = NG * TN * 16;
-  static constexpr int NWF = TN * 9 * NCH;                 // weight fragments per wave
-  static_assert(NWF <= 36, "144 weight VGPRs per wave at most");
+  static_assert(TN * 9 * NCH <= 36, "144 weight VGPRs per wave at most");
   static constexpr int NST = TN % 2 == 0 ? TM * TN / 2 : TM * TN;   // epilogue stores per wave per tile
 };
 
-// WAVE ROLES: wave = pg * NG + ng (group = wave >> 2: for PG = 2 the two pixel groups, for PG = 1 the
-// channel groups 0-3 / 4-7).  Tile = 4 images x TM output rows x 4 PG columns; block = one BN-channel
-// slice for the whole launch.
+// WAVE ROLES: wave = pg * NG + ng (stagger group = wave >> 2).  Tile = 4 images x TM output rows x 4 PG
+// columns; block = one BN-channel slice for the whole launch.
 // HOOK (microbenchmark builds only, scripts/convbench.hip variants 285-289; the ABI never accepts them):
 // 1 = no DMA waits in the loop, 2 = no DMA at all in the loop, 3 = no epilogue (results kept alive by a
-// store under a condition that never holds).
-template <int NCH, int TN, int TM, int PG, int NG, int NS, int ACT, int HOOK = 0>
+// store under a condition that never holds), 4 = DMA, waits and barriers only (no MFMA, no epilogue).
+template <int NCH, int TN, int TM, int PG, int NG, int NS, int STG, int ACT, int HOOK = 0>
 __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p, int nN) {
-  using G = S2Geo<NCH, TN, TM, PG, NG, NS>;
+  using G = S2Geo<NCH, TN, TM, PG, NG, NS, STG>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[G::LDS];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int ng = wave % NG, pg = wave / NG, grp = wave >> 2;
+  const int ng = wave % NG, pg = wave / NG, grp = STG ? (wave >> 2) : 0;
   const int g = lane >> 4, li = lane & 15;
 
   // block -> (N slice, virtual block of the pixel-tile walk): the nN blocks b, b + 8, ... of one XCD
@@ -105,8 +111,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
   const auto wr = make_rsrc(p.wf, p.wfbytes);
   const auto yr = make_rsrc(p.y, 0x7fffffffu);
 
-  // ---- the wave's weights, resident for the launch: fragment (nf, chunk c, tap) at ((nf * NCH + c) * 9 +
-  // tap) KiB of the packed copy, lane-linear; channels past cout read zeros (past wfbytes)
+  // ---- the wave's weights, resident for the launch: fragment (nf, K step c, tap) at ((nf * NCH + c) *
+  // 9 + tap) KiB of the packed copy, lane-linear; channels past cout read zeros (past wfbytes)
   u4 wreg[TN][9 * NCH];
 #pragma unroll
   for (int j = 0; j < TN; ++j) {
@@ -123,20 +129,21 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
     for (int e = 0; e < 4; ++e) bias[j][e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
   }
 
-  // ---- DMA pieces of this wave: piece k = wave + 8 m; lane -> storage pixel 16 k + lane / 4 (image,
-  // row, slot), 16-byte position lane % 4 holding source chunk (lane % 4) ^ f(image).  rel[m] = the
-  // lane's source offset relative to the tile's first patch pixel (image b0, row 2 y0 - 1, column
-  // 2 x0 - 1); pieces past the patch read past every tensor (zeros into the slot's padding).
+  // ---- DMA pieces of this wave: piece k = wave + 8 m; lane -> storage pixel 8 k + lane / 8 (image, row,
+  // slot) and LDS position lane % 8, which holds the pixel's source part (lane % 8) ^ pswz(slot) of the
+  // chunk's 128-byte line.  rel[m] = the lane's source offset relative to the tile's first patch pixel
+  // (image b0, row 2 y0 - 1, column 2 x0 - 1); pieces past the patch read past every tensor (zeros into
+  // the slot's padding).
   uint32_t rel[G::PW];
   const uint32_t rowb = (uint32_t)(p.W + 2) * p.xc * 2, imgb = (uint32_t)(p.H + 2) * rowb;
 #pragma unroll
   for (int m = 0; m < G::PW; ++m) {
-    const int sp = (wave + 8 * m) * 16 + (lane >> 2);
+    const int sp = (wave + 8 * m) * 8 + (lane >> 3);
     if (sp < G::PPX) {
       const int img = sp / (G::PR * G::PC), r2 = sp - img * (G::PR * G::PC);
       const int row = r2 / G::PC, slot = r2 - row * G::PC;
       const int pc = slot < G::NEV ? 2 * slot : 2 * (slot - G::NEV) + 1;
-      rel[m] = img * imgb + row * rowb + (uint32_t)((pc * p.xc + ((lane & 3) ^ swz(img)) * 8) * 2);
+      rel[m] = img * imgb + row * rowb + (uint32_t)((pc * p.xc + ((lane & 7) ^ pswz(slot)) * 8) * 2);
     } else {
       rel[m] = OOB;
     }
@@ -149,42 +156,63 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
     const int y0 = (t % nrg) * TM, b0 = (t / nrg) * FI;
     return (uint32_t)(pix_index(b0, 2 * y0 - 1, 2 * cg * FC * PG - 1, p.H, p.W) * p.xc * 2) + xoffb;
   };
-  // issue the wave's pieces of chunk q (flattened over the block's tiles) into ring slot q % NS; chunks
-  // past the last tile read past the tensor (their slots are never read again)
-  auto issue = [&](int q) __attribute__((always_inline)) {
-    if constexpr (HOOK == 2) return;
-    const int it = q / NCH, c = q - it * NCH;
+  // the wave's pieces m0 .. m1 - 1 of chunk q (flattened over the block's tiles) into ring slot q % NS;
+  // chunks past the last tile read past the tensor (their slots are never read again)
+  struct Src { uint32_t tb, so; unsigned char* dst; };
+  auto src_of = [&](int q) __attribute__((always_inline)) {
+    const int it = q / G::NDC, dc = q - it * G::NDC;
     const bool live = it < ntl;
-    const uint32_t tb = live ? tile_base(it) : OOB;
-    unsigned char* dst = smem + (q % NS) * G::SB + wave * 1024;
-#pragma unroll
-    for (int m = 0; m < G::PW; ++m) dma16(xr, dst + m * 8 * 1024, live ? tb + rel[m] : OOB, (uint32_t)(c * CK * 2));
+    return Src{live ? tile_base(it) : OOB, (uint32_t)(dc * DC * 2), smem + (q % NS) * G::SB + wave * 1024};
   };
+  auto issue_part = [&](const Src& sr, int m0, int m1) __attribute__((always_inline)) {
+    if constexpr (HOOK == 2) return;
+#pragma unroll
+    for (int m = 0; m < G::PW; ++m)
+      if (m >= m0 && m < m1) dma16(xr, sr.dst + m * 8 * 1024, sr.tb == OOB ? OOB : sr.tb + rel[m], sr.so);
+  };
+  auto issue = [&](int q) __attribute__((always_inline)) { issue_part(src_of(q), 0, G::PW); };
 
-  // ---- per-lane LDS read offset: image li / 4, column 4 pg + li % 4 of the fragment, position g ^ f(img)
-  const int img = li >> 2;
-  const uint32_t a_lane = (uint32_t)(((img * G::PR) * G::PC + FC * pg + (li & 3)) * 64 + ((g ^ swz(img)) * 16));
+  // ---- per-lane LDS read offsets: image li / 4, column slot 4 pg + SOFF[s] + li % 4 of the fragment;
+  // K-step half h's part g at position (4 h + g) ^ pswz(slot) (4 pg does not change slot & 3)
   constexpr int SOFF[3] = {0, G::NEV, 1};   // slot of column 2x + s relative to column 2x's
-
-  f4 acc[TN][TM];
-  // one chunk: three column steps; step s reads the 2 TM + 1 patch rows at column slot 4 pg + li % 4 +
-  // SOFF[s] once, output row i's tap (r, s) taking row 2 i + r
-  auto compute = [&](int q, int c) __attribute__((always_inline)) {
-    const unsigned char* pb = smem + (q % NS) * G::SB + a_lane;
+  const int img = li >> 2;
+  uint32_t a_off[2][3];
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
-      const unsigned char* ps = pb + SOFF[s] * 64;
-      u4 xa[G::PR];
+      const int slot = FC * pg + SOFF[s] + (li & 3);
+      a_off[h][s] = (uint32_t)(((img * G::PR) * G::PC + slot) * 128 + (((4 * h + g) ^ pswz(slot)) * 16));
+    }
+
+  f4 acc[TN][TM];
+  // one DMA chunk = two K steps h; each: three column steps; step s reads the 2 TM + 1 patch rows at
+  // the column slot once, output row i's tap (r, s) taking row 2 i + r
+  // the DMA of chunk qn is issued in six parts, one before each column step (a burst of every piece at the
+  // interval start stalled the waves' issue until the pieces drained: DMA and MFMAs ran one after the
+  // other, 151 us = 71 us DMA alone + 56 us MFMAs alone + epilogue on 64->128 @320)
+  auto compute = [&](int q, int dc, const Src& nx) __attribute__((always_inline)) {
+    const unsigned char* pb = smem + (q % NS) * G::SB;
 #pragma unroll
-      for (int r = 0; r < G::PR; ++r) xa[r] = *reinterpret_cast<const u4*>(ps + r * G::PC * 64);
+    for (int h = 0; h < 2; ++h) {
+      const int c = dc * 2 + h;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
+      for (int s = 0; s < 3; ++s) {
+        const int t6 = h * 3 + s;
+        issue_part(nx, t6 * G::PW / 6, (t6 + 1) * G::PW / 6);
+        const unsigned char* ps = pb + a_off[h][s];
+        u4 xa[G::PR];
 #pragma unroll
-        for (int r = 0; r < 3; ++r)
+        for (int r = 0; r < G::PR; ++r) xa[r] = *reinterpret_cast<const u4*>(ps + r * G::PC * 128);
 #pragma unroll
-          for (int j = 0; j < TN; ++j)
-            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wreg[j][c * 9 + r * 3 + s]),
-                                                               __builtin_bit_cast(h8, xa[2 * i + r]), acc[j][i], 0, 0, 0);
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int r = 0; r < 3; ++r)
+#pragma unroll
+            for (int j = 0; j < TN; ++j)
+              acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wreg[j][c * 9 + r * 3 + s]),
+                                                                 __builtin_bit_cast(h8, xa[2 * i + r]), acc[j][i], 0, 0, 0);
+      }
     }
   };
   const uint32_t lane_ch = (uint32_t)(16 * (g & 1) + 8 * (g >> 1));
@@ -240,14 +268,14 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
   for (int q = 0; q < G::L; ++q) issue(q);
   vmwait<G::PW * (G::L - 1)>();   // (the weight loads are older: retired too)
   barrier();
-  if (grp == 1) {   // the stagger: group 1 runs one interval behind, issuing chunk L in its idle interval
+  if (STG && grp == 1) {   // the stagger: group 1 runs one interval behind, issuing chunk L in its idle interval
     issue(G::L);
     vmwait<G::PW * (G::L - 1)>();
     barrier();
   }
 
-  // ---- steady state: interval = [issue chunk q + L (+1 for group 1)][compute chunk q][epilogue at a
-  // tile end][wait for this wave's pieces of the chunk the next interval reads][barrier]
+  // ---- steady state: interval = [issue chunk q + L (+1 for stagger group 1)][compute chunk q][epilogue
+  // at a tile end][wait for this wave's pieces of the chunk the next interval reads][barrier]
   const int ahead = G::L + grp;
   for (int it = 0; it < ntl; ++it) {
 #pragma unroll
@@ -255,17 +283,18 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
 #pragma unroll
       for (int i = 0; i < TM; ++i) acc[j][i] = bias[j];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int q = it * NCH + c;
-      issue(q + ahead);
-      compute(q, c);
-      if (c == NCH - 1) {
+    for (int dc = 0; dc < G::NDC; ++dc) {
+      const int q = it * G::NDC + dc;
+      const Src nx = src_of(q + ahead);
+      if constexpr (HOOK != 4) compute(q, dc, nx);
+      else issue_part(nx, 0, G::PW);
+      if (dc == G::NDC - 1) {
         // the accumulators are final: keep the epilogue math out of the MFMA stream
 #pragma unroll
         for (int j = 0; j < TN; ++j)
 #pragma unroll
           for (int i = 0; i < TM; ++i) asm volatile("" : "+v"(acc[j][i]));
-        if constexpr (HOOK == 3) {
+        if constexpr (HOOK == 3 || HOOK == 4) {
           if (p.cout < 0) epilogue(it);
         } else {
           epilogue(it);
@@ -273,33 +302,34 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
       }
       // younger than the pieces the next interval needs (issued L - 1 intervals ago): the L - 1 later
       // piece batches and the epilogue stores of intervals q - L + 1 .. q (a tile end among them: this
-      // one, or for L = 2 and c = 0 the previous tile's last chunk)
+      // one, or for L = 2 the previous one — the previous tile's last chunk when dc == 0)
       if constexpr (HOOK == 1 || HOOK == 2) {
       } else if constexpr (G::L == 1) {
-        if (c == NCH - 1) vmwait<G::NST>();
+        if (dc == G::NDC - 1) vmwait<G::NST>();
         else vmwait<0>();
       } else {
-        if (c == NCH - 1) vmwait<G::PW + G::NST>();
-        else if (c == 0 && it > 0) vmwait<G::PW + G::NST>();
+        if (dc == G::NDC - 1) vmwait<G::PW + G::NST>();
+        else if (dc == 0 && it > 0) vmwait<G::PW + G::NST>();
         else vmwait<G::PW>();
       }
       barrier();
     }
   }
-  if (grp == 0) barrier();   // group 1's extra barrier
-  vmwait<0>();                // no DMA may land after the block's LDS is released
+  if (STG && grp == 0) barrier();   // group 1's extra barrier
+  vmwait<0>();                       // no DMA may land after the block's LDS is released
 }
 
-// tile configurations (variants 280 + row): {NCH, TN, TM, PG, NG, NS}
-#define S2_CFGS(X) \
-  X(0, 2, 2, 4, 2, 4, 4) X(1, 4, 1, 8, 1, 8, 4) X(2, 4, 1, 4, 1, 8, 4) X(3, 2, 2, 4, 2, 4, 3) X(4, 4, 1, 8, 1, 8, 3)
-#define S2_ROW(i, nch, tn, tm, pg, ng, ns) {nch, tn, tm, pg, ng, ns},
-constexpr int S2_CFG[][6] = {S2_CFGS(S2_ROW)};
+// tile configurations (variants 280 + row): {NCH, TN, TM, PG, NG, NS, STG}
+#define S2_CFGS(X)                                                                                       \
+  X(0, 2, 2, 2, 2, 4, 3, 0) X(1, 2, 2, 4, 2, 4, 2, 0) X(2, 4, 1, 4, 1, 8, 3, 0) X(3, 4, 1, 2, 1, 8, 4, 1) \
+  X(4, 4, 1, 8, 1, 8, 2, 0)
+#define S2_ROW(i, nch, tn, tm, pg, ng, ns, stg) {nch, tn, tm, pg, ng, ns, stg},
+constexpr int S2_CFG[][7] = {S2_CFGS(S2_ROW)};
 constexpr int S2_NCFG = sizeof(S2_CFG) / sizeof(S2_CFG[0]);
 
-template <int NCH, int TN, int TM, int PG, int NG, int NS, int HOOK = 0>
+template <int NCH, int TN, int TM, int PG, int NG, int NS, int STG, int HOOK = 0>
 hipError_t launch_cfg(const ConvParams& p, int cus, hipStream_t st) {
-  using G = S2Geo<NCH, TN, TM, PG, NG, NS>;
+  using G = S2Geo<NCH, TN, TM, PG, NG, NS, STG>;
   const int nN = (p.cout + G::BN - 1) / G::BN;
   const long T = (long)((p.B + FI - 1) / FI) * (p.Ho / TM) * (p.Wo / (FC * PG));
   // persistent grid: a multiple of 8 * nN blocks (each XCD holds every N slice of its walk), at most one
@@ -310,15 +340,15 @@ hipError_t launch_cfg(const ConvParams& p, int cus, hipStream_t st) {
   if (per < 1) per = 1;
   const int grid = (int)(per * 8 * nN);
   if (HOOK) {
-    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, 1, HOOK>), dim3(grid), dim3(512), 0, st, p, nN);
+    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, 1, HOOK>), dim3(grid), dim3(512), 0, st, p, nN);
     return hipGetLastError();
   }
   if (p.act == 1)
-    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, 1>), dim3(grid), dim3(512), 0, st, p, nN);
+    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, 1>), dim3(grid), dim3(512), 0, st, p, nN);
   else if (p.act == 2)
-    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, 2>), dim3(grid), dim3(512), 0, st, p, nN);
+    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, 2>), dim3(grid), dim3(512), 0, st, p, nN);
   else
-    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, 0>), dim3(grid), dim3(512), 0, st, p, nN);
+    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, 0>), dim3(grid), dim3(512), 0, st, p, nN);
   return hipGetLastError();
 }
 
@@ -328,26 +358,26 @@ hipError_t launch_cfg(const ConvParams& p, int cus, hipStream_t st) {
 bool s2_supported(const ConvParams& p, int cfg) {
   if (cfg < 0 || cfg >= S2_NCFG) return false;
   const int nch = S2_CFG[cfg][0], tm = S2_CFG[cfg][2], pg = S2_CFG[cfg][3];
-  return p.wf && p.k == 3 && p.s == 2 && p.pad == 1 && !p.pool && p.cin == nch * CK && p.H % 2 == 0 &&
+  return p.wf && p.k == 3 && p.s == 2 && p.pad == 1 && !p.pool && p.cin == nch * 32 && p.H % 2 == 0 &&
          p.W % 2 == 0 && p.Ho == p.H / 2 && p.Wo == p.W / 2 && p.Ho % tm == 0 && p.Wo % (FC * pg) == 0 &&
          p.cout % 16 == 0 && p.cout <= 1024 && p.xoff % 8 == 0 && p.xc % 8 == 0 && p.yoff % 8 == 0 && p.yc % 8 == 0;
 }
 
 hipError_t launch_conv_s2(const ConvParams& p, int cfg, int cus, hipStream_t st) {
   if (!s2_supported(p, cfg)) return hipErrorInvalidValue;
-  // microbenchmark hooks (convbench; p.variant 285-287: cfg 0 with HOOK 1-3, 288-289: cfg 2 with HOOK 1-2)
+  // microbenchmark hooks (convbench; p.variant 285-287: cfg 0 with HOOK 4, 2, 3; 288-289: cfg 2 with HOOK 4, 2)
   if (p.act == 1 && p.variant >= 285 && p.variant <= 287 && cfg == 0) {
-    if (p.variant == 285) return launch_cfg<2, 2, 4, 2, 4, 4, 1>(p, cus, st);
-    if (p.variant == 286) return launch_cfg<2, 2, 4, 2, 4, 4, 2>(p, cus, st);
-    return launch_cfg<2, 2, 4, 2, 4, 4, 3>(p, cus, st);
+    if (p.variant == 285) return launch_cfg<2, 2, 2, 2, 4, 3, 0, 4>(p, cus, st);
+    if (p.variant == 286) return launch_cfg<2, 2, 2, 2, 4, 3, 0, 2>(p, cus, st);
+    return launch_cfg<2, 2, 2, 2, 4, 3, 0, 3>(p, cus, st);
   }
   if (p.act == 1 && p.variant >= 288 && p.variant <= 289 && cfg == 2) {
-    if (p.variant == 288) return launch_cfg<4, 1, 4, 1, 8, 4, 1>(p, cus, st);
-    return launch_cfg<4, 1, 4, 1, 8, 4, 2>(p, cus, st);
+    if (p.variant == 288) return launch_cfg<4, 1, 4, 1, 8, 3, 0, 4>(p, cus, st);
+    return launch_cfg<4, 1, 4, 1, 8, 3, 0, 2>(p, cus, st);
   }
   switch (cfg) {
-#define S2_CASE(i, nch, tn, tm, pg, ng, ns) \
-  case i: return launch_cfg<nch, tn, tm, pg, ng, ns>(p, cus, st);
+#define S2_CASE(i, nch, tn, tm, pg, ng, ns, stg) \
+  case i: return launch_cfg<nch, tn, tm, pg, ng, ns, stg>(p, cus, st);
     S2_CFGS(S2_CASE)
 #undef S2_CASE
   }
