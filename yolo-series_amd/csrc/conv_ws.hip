@@ -43,11 +43,9 @@ constexpr int PS = TS + 2;                   // patch side
 constexpr int PPIX = PS * PS;                // 324 patch pixels
 constexpr int PGROUPS = (PPIX + 7) / 8;      // 41 DMA wave-instructions (8 pixels x 128 B) per patch
 constexpr int PBUF = PGROUPS * 1024;         // 41,984 B per patch buffer
-constexpr int GPW = (PGROUPS + 3) / 4;       // 11 DMA instructions per wave per patch
 constexpr int CI = 64, CO = 64;
 constexpr int WTAP = CO * CI * 2;            // 8 KiB of weights per tap
 constexpr int LDS = 2 * PBUF + 9 * WTAP;     // 157,696 B
-constexpr int NSTORE = 8;                    // epilogue stores per lane per tile
 typedef uint32_t u2 __attribute__((ext_vector_type(2)));
 
 __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint32_t vo, uint32_t so) {

@@ -639,7 +639,7 @@ constexpr int NT_RG = 512;
 
 template <typename S, int ACT_A, int ACT_B>
 __global__ __launch_bounds__(NT_RG, 1) void stem_reorg_kernel(const StemParams p) {
-  constexpr int CA = 64, CB = 128, TBY = 4, TBX = 16;
+  constexpr int CA = 64, TBY = 4, TBX = 16;   // (conv B: 128 channels)
   constexpr int TAY = 2 * TBY + 1, TAX = 2 * TBX + 1;   // conv-A pixels feeding the tile: 9 x 33
   constexpr int NA = TAY * TAX;                          // 297
   constexpr int MA = 20;                                 // conv-A m-tiles (padded)
