@@ -54,6 +54,11 @@ int main(int argc, char** argv) {
     {"3x3s2 512->512 @40", 32, 40, 40, 512, 512, 3, 2},
     {"3x3s2 128->256 @320 b8", 8, 320, 320, 128, 256, 3, 2},
     {"3x3s2 128->256 @160 b8", 8, 160, 160, 128, 256, 3, 2},
+    {"3x3s2 256->512 @160 b8", 8, 160, 160, 256, 512, 3, 2},
+    {"3x3s2 512->768 @80 b8", 8, 80, 80, 512, 768, 3, 2},
+    {"3x3s2 768->1024 @40 b8", 8, 40, 40, 768, 1024, 3, 2},
+    {"3x3s2 256->384 @80 b8", 8, 80, 80, 256, 384, 3, 2},
+    {"3x3s2 384->512 @40 b8", 8, 40, 40, 384, 512, 3, 2},
     {"3x3 128->256 @80", 32, 80, 80, 128, 256, 3, 1},
     {"3x3 256->512 @40", 32, 40, 40, 256, 512, 3, 1},
     {"3x3 512->1024 @20", 32, 20, 20, 512, 1024, 3, 1},

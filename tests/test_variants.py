@@ -10,7 +10,7 @@ splits (1CS: configuration C, S splits; the split-K hand-off of splitk_reduce), 
 (201-206), the 8-phase rings (231: 256 x 256, 232: 256 x 128), the weight-stationary 1x1 rings (234-236,
 and 239: N-split), the column-group 3x3 halo ring (262), the
 low-resolution 3x3 kernel (270-273: 80 / 64-pixel tiles of 4 images x 4 columns, 128 / 64 channels;
-274: stride 2; 275 / 276: 160-pixel tiles), the register-weight stride-2 kernel (280-284: cin 64 / 128,
+274 / 277-279: stride 2; 275 / 276: 160-pixel tiles), the register-weight stride-2 kernel (280-284: cin 64 / 128,
 4 or 3 ring slots, 4 / 8-row tiles) and
 the alternative Detect heads (92, 97, and 99: the 64 x 256 ring that was the default before the
 persistent head).  A variant a layer's shape
@@ -30,7 +30,7 @@ DEV = 'cuda:0'
 CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15, 17,
                  100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
                  201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274, 275, 276,
-                 280, 281, 282, 283, 284]
+                 277, 278, 279, 280, 281, 282, 283, 284]
 DET_VARIANTS = [92, 97, 99]
 
 
@@ -99,7 +99,7 @@ def test_fragment_kernels_ragged(B):
     x = frames(B, H, W, seed=7).to(DEV).half()
     convs = [i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV]
     lines = []
-    for v in [0, 270, 271, 272, 273, 274, 275, 276, 280, 281, 282, 283, 284]:
+    for v in [0, 270, 271, 272, 273, 274, 275, 276, 277, 278, 279, 280, 281, 282, 283, 284]:
         for i in convs:
             plan.set_op_variant(i, v)
         z, xs = plan.forward(x)
@@ -119,7 +119,7 @@ def test_variant_api_rejects_hooks():
     plan = m.plan()
     conv = next(i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV)
     for v in (12, 13, 14, 16, 18, 19, 90, 91, 93, 94, 298, 160, 105, 211, 221, 233, 237, 238, 240, 241,
-              248, 255, 259, 260, 261, 263, 277, 911):
+              248, 255, 259, 260, 261, 263, 285, 289, 911):
         with pytest.raises(RuntimeError):
             plan.set_op_variant(conv, v)
     with pytest.raises(RuntimeError):

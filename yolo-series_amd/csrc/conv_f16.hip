@@ -2044,7 +2044,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   if (!det && (variant == 262 || (variant >= 911 && variant <= 914)) && hring_supported(p) && p.cout % 128 == 0)
     return launch_conv_hring(p, device_cus(), st);
   // the low-resolution 3x3 kernel (conv_lr.hip): 270 + tile configuration
-  if (!det && variant >= 270 && variant <= 276 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
+  if (!det && variant >= 270 && variant <= 279 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
   // the register-weight stride-2 kernel (conv_s2.hip): 280 + tile configuration
   if (!det && variant >= 280 && variant <= 284 && s2_supported(p, variant - 280))
     return launch_conv_s2(p, variant - 280, device_cus(), st);
@@ -2097,11 +2097,16 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // w6 bs 8 512->768 s2 @80 134.6 -> 107.6, 256->384 s2 @80 39.5 -> 35.7; yolov7 bs 32 512->512 s2 @40
   // p8n 76.8 vs 90.5 here)
   const long t2n_s2 = (long)((p.M + 255) / 256) * ((p.cout + 127) / 128);
+  // Round 5: the 80-pixel stride-2 tile (cfg 7, 5 output rows) on the 12 800-pixel layers with cout >= 384
+  // (one layer forced at a time, profiles/r5_s2/tune_deep_w6.txt, us, cfg 4 -> 7: yolov7-w6 bs 8 512->768
+  // s2 @80 109.1 -> 101.5, 256->384 s2 @80 37.7 -> 31.3; yolov7 bs 32 256->256 s2 @40 keeps cfg 4: 27.0
+  // vs 28.8)
   if (!det && variant == 0 && lr && p.k == 3 && p.s == 2 &&
       ((long)((p.M + 127) / 128) * ((p.cout + 127) / 128) <= 256 ||
-       (p.M <= 12800 && !(t2n_s2 >= 150 && t2n_s2 <= 250 && p.cout >= 512))) &&
-      lr_supported(p, 4))
-    return launch_conv_lr(p, 4, st);
+       (p.M <= 12800 && !(t2n_s2 >= 150 && t2n_s2 <= 250 && p.cout >= 512)))) {
+    const int cfg = (p.M >= 12800 && p.cout >= 384 && lr_supported(p, 7)) ? 7 : 4;
+    if (lr_supported(p, cfg)) return launch_conv_lr(p, cfg, st);
+  }
   // 3x3 stride-1 layers with 128-channel output tiles and at least one round of 16 x 16 x 128 tiles: the
   // column-group halo ring (conv_hring.hip, variant 262).  Single-layer sweep, bs 32 640, same box
   // (profiles/r3_hring2_tune.txt, us, dispatch -> 262): 3x3 128->128 @80 80.0 / 80.4 / 82.7 / 81.0 ->

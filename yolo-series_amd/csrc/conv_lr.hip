@@ -309,12 +309,16 @@ hipError_t launch_nch(const ConvParams& p, hipStream_t st) {
 // vs 68: a 9-column, 2*TH+1-row patch per output tile is 4-5 input pixels per output against 2.1 at
 // stride 1) and faster only where the dispatch split K: 256->256 s2 @40 25.4 vs 29.6.  5 / 6: 160-pixel
 // tiles (TH = 10) of 128 / 64 channels (profiles/r4lr/tune_tm10*.txt: 3-9 % on the wide layers).
+// Round 5, stride 2 (profiles/r5_s2/cb_deep_s2.txt, tune_deep_*.txt): 7 = 80 x 128 (5 rows) wins on the
+// w6 12 800-pixel layers with cout >= 384 (512->768 s2 @80 109.1 -> 101.5 us in-network); 8 = 128 x 128
+// (8 rows, PD 2) and 9 = 160 x 64 lost everywhere (VGPR-bound weight prefetch, LDS-read bound) and are
+// kept only as forced variants.
 // Reading the next column step's patch rows before this step's MFMAs (two register sets; across a
 // chunk boundary after the barrier) was no faster on any layer and cost a wave per SIMD
 // (profiles/r4lr/tune_xp.txt): three waves per SIMD already hide the LDS latency.
 #define LR_CFGS(X)                                                                                   \
   X(0, 1, 4, 2, 5, 3, 1) X(1, 1, 4, 1, 5, 3, 1) X(2, 1, 4, 2, 4, 3, 1) X(3, 1, 4, 1, 4, 3, 1) X(4, 1, 4, 2, 4, 3, 2) \
-  X(5, 1, 4, 2, 10, 2, 1) X(6, 1, 4, 1, 10, 3, 1)
+  X(5, 1, 4, 2, 10, 2, 1) X(6, 1, 4, 1, 10, 3, 1) X(7, 1, 4, 2, 5, 3, 2) X(8, 1, 4, 2, 8, 2, 2) X(9, 1, 4, 1, 10, 3, 2)
 #define LR_ROW(i, wm, wn, tn, tm, pd, s) {wm, wn, tn, tm, pd, s},
 constexpr int LR_CFG[][6] = {LR_CFGS(LR_ROW)};
 constexpr int LR_NCFG = sizeof(LR_CFG) / sizeof(LR_CFG[0]);
