@@ -11,7 +11,8 @@ splits (1CS: configuration C, S splits; the split-K hand-off of splitk_reduce), 
 and 239: N-split), the column-group 3x3 halo ring (262), the
 low-resolution 3x3 kernel (270-273: 80 / 64-pixel tiles of 4 images x 4 columns, 128 / 64 channels;
 274 / 277-279: stride 2; 275 / 276: 160-pixel tiles), the register-weight stride-2 kernel (280-284: cin 64 / 128,
-4 or 3 ring slots, 4 / 8-row tiles) and
+4 or 3 ring slots, 4 / 8-row tiles), the register-weight 1x1 kernel (290-295: cin 128 / 256 / 512, with and
+without the stagger) and
 the alternative Detect heads (92, 97, and 99: the 64 x 256 ring that was the default before the
 persistent head).  A variant a layer's shape
 does not support falls back to the tuned kernel, which the check then covers again.
@@ -30,7 +31,7 @@ DEV = 'cuda:0'
 CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15, 17,
                  100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
                  201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274, 275, 276,
-                 277, 278, 279, 280, 281, 282, 283, 284]
+                 277, 278, 279, 280, 281, 282, 283, 284, 290, 291, 292, 293, 294, 295]
 DET_VARIANTS = [92, 97, 99]
 
 
@@ -86,8 +87,8 @@ RAGGED = {'nc': 3, 'depth_multiple': 1.0, 'width_multiple': 1.0,
 
 @pytest.mark.parametrize('B', [5, 6])
 def test_fragment_kernels_ragged(B):
-    """The fragment kernels (conv_lr.hip 270-276, conv_s2.hip 280-284) on partial trailing image groups
-    and half-masked channel pairs, op by op against fp32 torch."""
+    """The fragment kernels (conv_lr.hip 270-279, conv_s2.hip 280-284, conv_w1.hip 290-295) on partial
+    trailing image groups / pixel tiles and half-masked channel pairs, op by op against fp32 torch."""
     import copy
     from models.yolo import Model
     from yv7.synthetic import synthetic_state_dict
@@ -99,7 +100,8 @@ def test_fragment_kernels_ragged(B):
     x = frames(B, H, W, seed=7).to(DEV).half()
     convs = [i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV]
     lines = []
-    for v in [0, 270, 271, 272, 273, 274, 275, 276, 277, 278, 279, 280, 281, 282, 283, 284]:
+    for v in [0, 270, 271, 272, 273, 274, 275, 276, 277, 278, 279, 280, 281, 282, 283, 284, 290, 291, 292, 293,
+              294, 295]:
         for i in convs:
             plan.set_op_variant(i, v)
         z, xs = plan.forward(x)

@@ -2050,6 +2050,10 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     return launch_conv_s2(p, variant - 280, device_cus(), st);
   if (!det && variant >= 285 && variant <= 289 && s2_supported(p, variant <= 287 ? 0 : 2))   // its hooks (convbench)
     return launch_conv_s2(p, variant <= 287 ? 0 : 2, device_cus(), st);
+  // the register-weight 1x1 kernel (conv_w1.hip): 290 + configuration
+  if (!det && variant >= 290 && variant <= 295 && w1_supported(p, variant - 290))
+    return launch_conv_w1(p, variant - 290, device_cus(), st);
+  if (!det && variant >= 299 && variant <= 301 && w1_supported(p, 1)) return launch_conv_w1(p, 1, device_cus(), st);   // its hooks
   // 3x3 stride-1 layers of up to 204 800 output pixels (yolov7 640 bs 32 from 80^2 down, yolov7-w6 1280
   // bs 8 from 160^2 down): the low-resolution kernel (conv_lr.hip) — one layer forced at a time in the bs-32
   // forward (profiles/r4lr/tune3.txt, us, dispatch -> lr): 3x3 256->256 @20 32.2 -> 22.1, 512->512 @20
@@ -2088,6 +2092,20 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   if (!det && variant == 0 && s2k && p.k == 3 && p.s == 2 && (long)p.M >= 204800 && (p.cin == 64 || p.cin == 128)) {
     const int cfg = p.cin == 64 ? 0 : (p.cout >= 256 ? 4 : 3);
     if (s2_supported(p, cfg)) return launch_conv_s2(p, cfg, device_cus(), st);
+  }
+  // 1x1 stride-1 layers with 128 / 256 / 512 inputs: the register-weight 1x1 kernel (conv_w1.hip).  In-
+  // network, one layer forced at a time (scripts/tune_ops.py, profiles/r5_w1/tune_*.txt, us, dispatch ->
+  // w1): yolov7 bs 32 128->128 @160 87.5 -> 75.2 (cfg 0), 256->256 @160 187.5 -> 163.5, @80 58.3 -> 49.1
+  // (cfg 3), 512->512 @80 147.5 -> 119.9, @40 47.6 -> 39.6 (cfg 5), 512->384 @80 131.1 -> 113.1 (cfg 2);
+  // yolov7-w6 bs 8 128->128 @320 91.3 -> 73.3, 512->256 @160 90.7 -> 65.5.  Narrower grids keep the
+  // rings below.  YV7_W1=0: off.
+  static const int w1k = [] { const char* e = getenv("YV7_W1"); return e ? atoi(e) : 1; }();
+  if (!det && variant == 0 && w1k && one && !p.pool) {
+    int cfg = -1;
+    if (p.cin == 128 && p.M >= 409600) cfg = 0;
+    else if (p.cin == 256 && p.M >= 204800) cfg = 3;
+    else if (p.cin == 512 && p.M >= 51200) cfg = p.cout % 256 == 0 ? 5 : (p.M >= 204800 ? 2 : -1);
+    if (cfg >= 0 && w1_supported(p, cfg)) return launch_conv_w1(p, cfg, device_cus(), st);
   }
   // 3x3 stride-2 layers the 128 x 128 ring would split K for (under 256 of its tiles: yolov7's 256->256
   // s2 @40, w6's 768->1024 s2 @40): the stride-2 low-resolution form (profiles/r4lr/convbench_s2.txt:

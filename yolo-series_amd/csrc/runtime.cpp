@@ -115,16 +115,19 @@ int kpad_of(const yv7_op_desc& o) {
 bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7_WFMT_FP8; }
 // 3x3 / stride-1 or 2 / pad-1 fp16 convs of a shape the fragment kernels accept (conv_lr.hip lr_supported:
 // cin / 32 in {2, 4, 6, 8, 12, 16, 24}, cout % 16 == 0, cout <= 1024; conv_s2.hip: cin 64 / 128) get a
-// fragment-packed weight copy — none at all with YV7_LR=0 (the fragment kernels then never run: the
-// forced variants 270-276 / 280-284 fall back to the tuned kernel).  yolov7: 36.9 MB, yolov7-w6: 60.5 MB
+// fragment-packed weight copy, and so do 1x1 stride-1 convs with 128 / 256 / 512 inputs (conv_w1.hip) —
+// none at all with YV7_LR=0 (the fragment kernels then never run: the forced variants 270-284 / 290-295
+// fall back to the tuned kernel).  yolov7: 36.9 MB, yolov7-w6: 60.5 MB
 // per fp16 plan.
 bool wants_frag(int dtype, const yv7_op_desc& o) {
   static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
   const int nch = o.cin / 32;
-  return lr && dtype == YV7_DT_F16 && o.kind == YV7_OP_CONV && !is_f8(o) && o.k == 3 && (o.s == 1 || o.s == 2) &&
-         o.pad == 1 && !o.pool && o.cin % 32 == 0 &&
-         (nch == 2 || nch == 4 || nch == 6 || nch == 8 || nch == 12 || nch == 16 || nch == 24) && o.cout % 16 == 0 &&
-         o.cout <= 1024;
+  if (!lr || dtype != YV7_DT_F16 || o.kind != YV7_OP_CONV || is_f8(o) || o.pool || o.cout % 16 || o.cout > 1024)
+    return false;
+  if (o.k == 1)   // conv_w1.hip: 1x1 stride 1 with 128 / 256 / 512 inputs
+    return o.s == 1 && o.pad == 0 && (o.cin == 128 || o.cin == 256 || o.cin == 512);
+  return o.k == 3 && (o.s == 1 || o.s == 2) && o.pad == 1 && o.cin % 32 == 0 &&
+         (nch == 2 || nch == 4 || nch == 6 || nch == 8 || nch == 12 || nch == 16 || nch == 24);
 }
 
 // Geometry / operand fields of a CONV or DETECT op's kernel parameters (pointers into the workspace
@@ -415,7 +418,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15 || v == 17) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
   return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
-         (v >= 270 && v <= 284);
+         (v >= 270 && v <= 284) || (v >= 290 && v <= 295);
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {

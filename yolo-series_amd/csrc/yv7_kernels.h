@@ -217,6 +217,9 @@ hipError_t launch_conv_hring(const ConvParams& p, int cus, hipStream_t st);
 // stride-2 3x3 with the weights resident in VGPRs (conv_s2.hip): cfg 0-4 = tile shape; weights from wf
 bool s2_supported(const ConvParams& p, int cfg);
 hipError_t launch_conv_s2(const ConvParams& p, int cfg, int cus, hipStream_t st);
+// 1x1 with the weights resident in VGPRs (conv_w1.hip): cfg 0-5; weights from wf (1-tap fragment pack)
+bool w1_supported(const ConvParams& p, int cfg);
+hipError_t launch_conv_w1(const ConvParams& p, int cfg, int cus, hipStream_t st);
 hipError_t launch_input(int dtype, const void* x, int x_dtype, void* y, int B, int H, int W, int yc,
                         bool reorg, hipStream_t st);
 hipError_t launch_maxpool(int dtype, const void* x, int B, int H, int W, int xc, int xoff, void* y, int Ho,
