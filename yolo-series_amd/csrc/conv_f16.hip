@@ -2046,10 +2046,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // the low-resolution 3x3 kernel (conv_lr.hip): 270 + tile configuration
   if (!det && variant >= 270 && variant <= 279 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
   // the register-weight stride-2 kernel (conv_s2.hip): 280 + tile configuration
-  if (!det && variant >= 280 && variant <= 284 && s2_supported(p, variant - 280))
+  if (!det && variant >= 280 && variant <= 288 && s2_supported(p, variant - 280))
     return launch_conv_s2(p, variant - 280, device_cus(), st);
-  if (!det && variant >= 285 && variant <= 289 && s2_supported(p, variant <= 287 ? 0 : 2))   // its hooks (convbench)
-    return launch_conv_s2(p, variant <= 287 ? 0 : 2, device_cus(), st);
   // the register-weight 1x1 kernel (conv_w1.hip): 290 + configuration
   if (!det && variant >= 290 && variant <= 295 && w1_supported(p, variant - 290))
     return launch_conv_w1(p, variant - 290, device_cus(), st);

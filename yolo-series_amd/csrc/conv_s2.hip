@@ -54,19 +54,24 @@ __device__ __forceinline__ void dma16(__amdgpu_buffer_rsrc_t r, void* lds, uint3
   __builtin_amdgcn_raw_ptr_buffer_load_lds(r, (__attribute__((address_space(3))) void*)lds, 16, vo, so, 0, 0);
 }
 
-// position swizzle of a pixel's eight 16-byte parts by its column slot
-__host__ __device__ constexpr int pswz(int slot) { return 2 * (slot & 3); }
+// position swizzle of a pixel's eight 16-byte parts (S = 2: by its column slot; S = 1, whose patch rows
+// have an even pixel count, by image and slot — scripts/s2_swizzle_check.py, s1_swizzle_check.py)
+template <int S>
+__host__ __device__ constexpr int pswz(int img, int slot) {
+  return S == 2 ? 2 * (slot & 3) : 2 * ((img >> 1) & 1) ^ 4 * ((slot >> 1) & 1);
+}
 
 // Compile-time geometry of one configuration.  NCH = cin / 32 (MFMA K steps per tap).
-template <int NCH, int TN, int TM, int PG, int NG, int NS, int STG>
+template <int NCH, int TN, int TM, int PG, int NG, int NS, int STG, int S>
 struct S2Geo {
   static constexpr int NW = NG * PG;                       // waves
   static_assert(NW == 8, "eight waves");
   static_assert(NCH % 2 == 0, "whole 64-channel DMA chunks");
   static constexpr int NDC = NCH / 2;                      // DMA chunks per tile
-  static constexpr int PR = 2 * TM + 1;                    // patch rows
-  static constexpr int NEV = 4 * PG + 1;                   // even patch columns (slots 0 .. NEV - 1)
-  static constexpr int PC = 8 * PG + 1;                    // patch columns
+  static_assert(S == 1 || S == 2, "stride");
+  static constexpr int PR = S == 2 ? 2 * TM + 1 : TM + 2;  // patch rows
+  static constexpr int NEV = 4 * PG + 1;                   // S = 2: even patch columns (slots 0 .. NEV - 1)
+  static constexpr int PC = S == 2 ? 8 * PG + 1 : 4 * PG + 2;   // patch columns
   static constexpr int PPX = FI * PR * PC;                 // patch pixels
   static constexpr int NP = (PPX + 7) / 8;                 // 1 KiB DMA pieces (8 pixels x 128 B)
   static constexpr int PW = (NP + NW - 1) / NW;            // pieces per wave per chunk
@@ -82,12 +87,12 @@ struct S2Geo {
 
 // WAVE ROLES: wave = pg * NG + ng (stagger group = wave >> 2).  Tile = 4 images x TM output rows x 4 PG
 // columns; block = one BN-channel slice for the whole launch.
-// HOOK (microbenchmark builds only, scripts/convbench.hip variants 285-289; the ABI never accepts them):
+// HOOK (microbenchmark builds only — round 5 reached them as convbench variants 285-289; no longer mapped):
 // 1 = no DMA waits in the loop, 2 = no DMA at all in the loop, 3 = no epilogue (results kept alive by a
 // store under a condition that never holds), 4 = DMA, waits and barriers only (no MFMA, no epilogue).
-template <int NCH, int TN, int TM, int PG, int NG, int NS, int STG, int ACT, int HOOK = 0>
+template <int NCH, int TN, int TM, int PG, int NG, int NS, int STG, int S, int ACT, int HOOK = 0>
 __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p, int nN) {
-  using G = S2Geo<NCH, TN, TM, PG, NG, NS, STG>;
+  using G = S2Geo<NCH, TN, TM, PG, NG, NS, STG, S>;
   __shared__ __attribute__((aligned(16))) unsigned char smem[G::LDS];
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -142,8 +147,8 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
     if (sp < G::PPX) {
       const int img = sp / (G::PR * G::PC), r2 = sp - img * (G::PR * G::PC);
       const int row = r2 / G::PC, slot = r2 - row * G::PC;
-      const int pc = slot < G::NEV ? 2 * slot : 2 * (slot - G::NEV) + 1;
-      rel[m] = img * imgb + row * rowb + (uint32_t)((pc * p.xc + ((lane & 7) ^ pswz(slot)) * 8) * 2);
+      const int pc = S == 1 ? slot : (slot < G::NEV ? 2 * slot : 2 * (slot - G::NEV) + 1);
+      rel[m] = img * imgb + row * rowb + (uint32_t)((pc * p.xc + ((lane & 7) ^ pswz<S>(img, slot)) * 8) * 2);
     } else {
       rel[m] = OOB;
     }
@@ -154,7 +159,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
     const int cg = t % ncg;
     t /= ncg;
     const int y0 = (t % nrg) * TM, b0 = (t / nrg) * FI;
-    return (uint32_t)(pix_index(b0, 2 * y0 - 1, 2 * cg * FC * PG - 1, p.H, p.W) * p.xc * 2) + xoffb;
+    return (uint32_t)(pix_index(b0, S * y0 - 1, S * cg * FC * PG - 1, p.H, p.W) * p.xc * 2) + xoffb;
   };
   // the wave's pieces m0 .. m1 - 1 of chunk q (flattened over the block's tiles) into ring slot q % NS;
   // chunks past the last tile read past the tensor (their slots are never read again)
@@ -174,7 +179,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
 
   // ---- per-lane LDS read offsets: image li / 4, column slot 4 pg + SOFF[s] + li % 4 of the fragment;
   // K-step half h's part g at position (4 h + g) ^ pswz(slot) (4 pg does not change slot & 3)
-  constexpr int SOFF[3] = {0, G::NEV, 1};   // slot of column 2x + s relative to column 2x's
+  constexpr int SOFF[3] = {0, S == 2 ? G::NEV : 1, S == 2 ? 1 : 2};   // slot of column S x + s relative to S x's
   const int img = li >> 2;
   uint32_t a_off[2][3];
 #pragma unroll
@@ -182,7 +187,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
 #pragma unroll
     for (int s = 0; s < 3; ++s) {
       const int slot = FC * pg + SOFF[s] + (li & 3);
-      a_off[h][s] = (uint32_t)(((img * G::PR) * G::PC + slot) * 128 + (((4 * h + g) ^ pswz(slot)) * 16));
+      a_off[h][s] = (uint32_t)(((img * G::PR) * G::PC + slot) * 128 + (((4 * h + g) ^ pswz<S>(img, slot)) * 16));
     }
 
   f4 acc[TN][TM];
@@ -211,7 +216,7 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
 #pragma unroll
             for (int j = 0; j < TN; ++j)
               acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wreg[j][c * 9 + r * 3 + s]),
-                                                                 __builtin_bit_cast(h8, xa[2 * i + r]), acc[j][i], 0, 0, 0);
+                                                                 __builtin_bit_cast(h8, xa[S * i + r]), acc[j][i], 0, 0, 0);
       }
     }
   };
@@ -319,17 +324,20 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
   vmwait<0>();                       // no DMA may land after the block's LDS is released
 }
 
-// tile configurations (variants 280 + row): {NCH, TN, TM, PG, NG, NS, STG}
-#define S2_CFGS(X)                                                                                       \
-  X(0, 2, 2, 2, 2, 4, 3, 0) X(1, 2, 2, 4, 2, 4, 2, 0) X(2, 4, 1, 4, 1, 8, 3, 0) X(3, 4, 1, 2, 1, 8, 4, 1) \
-  X(4, 4, 1, 8, 1, 8, 2, 0)
-#define S2_ROW(i, nch, tn, tm, pg, ng, ns, stg) {nch, tn, tm, pg, ng, ns, stg},
-constexpr int S2_CFG[][7] = {S2_CFGS(S2_ROW)};
+// tile configurations (variants 280 + row): {NCH, TN, TM, PG, NG, NS, STG, S}.  0-4: stride 2 (cin 64 /
+// 128); 5-8: stride 1 (the same machinery for the 64 / 128-input 3x3 layers: cin 64 with 64 output
+// channels = conv_ws.hip's layers, cin 128).
+#define S2_CFGS(X)                                                                                             \
+  X(0, 2, 2, 2, 2, 4, 3, 0, 2) X(1, 2, 2, 4, 2, 4, 2, 0, 2) X(2, 4, 1, 4, 1, 8, 3, 0, 2) X(3, 4, 1, 2, 1, 8, 4, 1, 2) \
+  X(4, 4, 1, 8, 1, 8, 2, 0, 2) X(5, 2, 2, 2, 4, 2, 4, 1, 1) X(6, 2, 2, 4, 4, 2, 2, 0, 1) X(7, 4, 1, 4, 1, 8, 4, 1, 1) \
+  X(8, 4, 1, 8, 1, 8, 4, 1, 1)
+#define S2_ROW(i, nch, tn, tm, pg, ng, ns, stg, st) {nch, tn, tm, pg, ng, ns, stg, st},
+constexpr int S2_CFG[][8] = {S2_CFGS(S2_ROW)};
 constexpr int S2_NCFG = sizeof(S2_CFG) / sizeof(S2_CFG[0]);
 
-template <int NCH, int TN, int TM, int PG, int NG, int NS, int STG, int HOOK = 0>
+template <int NCH, int TN, int TM, int PG, int NG, int NS, int STG, int S, int HOOK = 0>
 hipError_t launch_cfg(const ConvParams& p, int cus, hipStream_t st) {
-  using G = S2Geo<NCH, TN, TM, PG, NG, NS, STG>;
+  using G = S2Geo<NCH, TN, TM, PG, NG, NS, STG, S>;
   const int nN = (p.cout + G::BN - 1) / G::BN;
   const long T = (long)((p.B + FI - 1) / FI) * (p.Ho / TM) * (p.Wo / (FC * PG));
   // persistent grid: a multiple of 8 * nN blocks (each XCD holds every N slice of its walk), at most one
@@ -340,15 +348,15 @@ hipError_t launch_cfg(const ConvParams& p, int cus, hipStream_t st) {
   if (per < 1) per = 1;
   const int grid = (int)(per * 8 * nN);
   if (HOOK) {
-    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, 1, HOOK>), dim3(grid), dim3(512), 0, st, p, nN);
+    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, S, 1, HOOK>), dim3(grid), dim3(512), 0, st, p, nN);
     return hipGetLastError();
   }
   if (p.act == 1)
-    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, 1>), dim3(grid), dim3(512), 0, st, p, nN);
+    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, S, 1>), dim3(grid), dim3(512), 0, st, p, nN);
   else if (p.act == 2)
-    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, 2>), dim3(grid), dim3(512), 0, st, p, nN);
+    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, S, 2>), dim3(grid), dim3(512), 0, st, p, nN);
   else
-    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, 0>), dim3(grid), dim3(512), 0, st, p, nN);
+    YV7_LAUNCH((conv3x3s2_rw_kernel<NCH, TN, TM, PG, NG, NS, STG, S, 0>), dim3(grid), dim3(512), 0, st, p, nN);
   return hipGetLastError();
 }
 
@@ -357,27 +365,19 @@ hipError_t launch_cfg(const ConvParams& p, int cus, hipStream_t st) {
 // cfg: S2_CFG row (variants 280 + cfg)
 bool s2_supported(const ConvParams& p, int cfg) {
   if (cfg < 0 || cfg >= S2_NCFG) return false;
-  const int nch = S2_CFG[cfg][0], tm = S2_CFG[cfg][2], pg = S2_CFG[cfg][3];
-  return p.wf && p.k == 3 && p.s == 2 && p.pad == 1 && !p.pool && p.cin == nch * 32 && p.H % 2 == 0 &&
-         p.W % 2 == 0 && p.Ho == p.H / 2 && p.Wo == p.W / 2 && p.Ho % tm == 0 && p.Wo % (FC * pg) == 0 &&
-         p.cout % 16 == 0 && p.cout <= 1024 && p.xoff % 8 == 0 && p.xc % 8 == 0 && p.yoff % 8 == 0 && p.yc % 8 == 0;
+  const int nch = S2_CFG[cfg][0], tm = S2_CFG[cfg][2], pg = S2_CFG[cfg][3], S = S2_CFG[cfg][7];
+  const bool geom = S == 2 ? (p.H % 2 == 0 && p.W % 2 == 0 && p.Ho == p.H / 2 && p.Wo == p.W / 2)
+                           : (p.Ho == p.H && p.Wo == p.W);
+  return p.wf && p.k == 3 && p.s == S && p.pad == 1 && !p.pool && p.cin == nch * 32 && geom && p.Ho % tm == 0 &&
+         p.Wo % (FC * pg) == 0 && p.cout % 16 == 0 && p.cout <= 1024 && p.xoff % 8 == 0 && p.xc % 8 == 0 &&
+         p.yoff % 8 == 0 && p.yc % 8 == 0;
 }
 
 hipError_t launch_conv_s2(const ConvParams& p, int cfg, int cus, hipStream_t st) {
   if (!s2_supported(p, cfg)) return hipErrorInvalidValue;
-  // microbenchmark hooks (convbench; p.variant 285-287: cfg 0 with HOOK 4, 2, 3; 288-289: cfg 2 with HOOK 4, 2)
-  if (p.act == 1 && p.variant >= 285 && p.variant <= 287 && cfg == 0) {
-    if (p.variant == 285) return launch_cfg<2, 2, 2, 2, 4, 3, 0, 4>(p, cus, st);
-    if (p.variant == 286) return launch_cfg<2, 2, 2, 2, 4, 3, 0, 2>(p, cus, st);
-    return launch_cfg<2, 2, 2, 2, 4, 3, 0, 3>(p, cus, st);
-  }
-  if (p.act == 1 && p.variant >= 288 && p.variant <= 289 && cfg == 2) {
-    if (p.variant == 288) return launch_cfg<4, 1, 4, 1, 8, 3, 0, 4>(p, cus, st);
-    return launch_cfg<4, 1, 4, 1, 8, 3, 0, 2>(p, cus, st);
-  }
   switch (cfg) {
-#define S2_CASE(i, nch, tn, tm, pg, ng, ns, stg) \
-  case i: return launch_cfg<nch, tn, tm, pg, ng, ns, stg>(p, cus, st);
+#define S2_CASE(i, nch, tn, tm, pg, ng, ns, stg, st_) \
+  case i: return launch_cfg<nch, tn, tm, pg, ng, ns, stg, st_>(p, cus, st);
     S2_CFGS(S2_CASE)
 #undef S2_CASE
   }

@@ -117,8 +117,8 @@ bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7
 // cin / 32 in {2, 4, 6, 8, 12, 16, 24}, cout % 16 == 0, cout <= 1024; conv_s2.hip: cin 64 / 128) get a
 // fragment-packed weight copy, and so do 1x1 stride-1 convs with 128 / 256 / 512 inputs (conv_w1.hip) —
 // none at all with YV7_LR=0 (the fragment kernels then never run: the forced variants 270-284 / 290-295
-// fall back to the tuned kernel).  yolov7: 36.9 MB, yolov7-w6: 60.5 MB
-// per fp16 plan.
+// fall back to the tuned kernel).  Per fp16 plan: yolov7 54.0 MB (3x3 49.8 + 1x1 4.1) beside its 73.9 MB
+// blob, yolov7-w6 112.4 MB, yolov7-tiny 10.3 MB.
 bool wants_frag(int dtype, const yv7_op_desc& o) {
   static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
   const int nch = o.cin / 32;
@@ -418,7 +418,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15 || v == 17) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
   return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
-         (v >= 270 && v <= 284) || (v >= 290 && v <= 295);
+         (v >= 270 && v <= 288) || (v >= 290 && v <= 295);
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {
