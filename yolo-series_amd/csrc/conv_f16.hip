@@ -2052,6 +2052,19 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   if (!det && variant >= 290 && variant <= 295 && w1_supported(p, variant - 290))
     return launch_conv_w1(p, variant - 290, device_cus(), st);
   if (!det && variant >= 299 && variant <= 301 && w1_supported(p, 1)) return launch_conv_w1(p, 1, device_cus(), st);   // its hooks
+  // The register-weight 3x3 kernel (conv_s2.hip) at stride 1, checked before the low-resolution rule
+  // below (which would take the 204 800-pixel layers).  In-network, one layer forced at a time
+  // (profiles/r5_s2/tune_s1_*.txt, us, dispatch -> s2 S=1): yolov7 bs 32 64->64 @320 228.2 -> 222.9
+  // (cfg 6), 128->128 @80 65.6 -> 62.2 / 65.0 -> 63.0 (cfg 7), 128->256 @80 116.2 -> 108.2 (cfg 8);
+  // yolov7-w6 bs 8 128->128 @160 68.4 -> 61.4, 128->256 @160 116.2 -> 106.5.  64->64 below 1 M pixels
+  // and the 64-output 128-input layers (57.1 vs 38.3) keep the dispatch below.  YV7_S1=0: off.
+  static const int s1k = [] { const char* e = getenv("YV7_S1"); return e ? atoi(e) : 1; }();
+  if (!det && variant == 0 && s1k && p.k == 3 && p.s == 1 && !p.pool && (long)p.M >= 204800) {
+    int cfg = -1;
+    if (p.cin == 64 && p.cout == 64 && (long)p.M >= 1000000) cfg = 6;
+    else if (p.cin == 128 && p.cout >= 128) cfg = p.cout >= 256 ? 8 : 7;
+    if (cfg >= 0 && s2_supported(p, cfg)) return launch_conv_s2(p, cfg, device_cus(), st);
+  }
   // 3x3 stride-1 layers of up to 204 800 output pixels (yolov7 640 bs 32 from 80^2 down, yolov7-w6 1280
   // bs 8 from 160^2 down): the low-resolution kernel (conv_lr.hip) — one layer forced at a time in the bs-32
   // forward (profiles/r4lr/tune3.txt, us, dispatch -> lr): 3x3 256->256 @20 32.2 -> 22.1, 512->512 @20
