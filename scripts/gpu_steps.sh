@@ -10,6 +10,7 @@
 #   tune=OPS:CANDS[:ROUNDS]     tune_ops.py: each candidate forced on one op at a time -> tune.txt
 #                               (OPS = all for every conv op)
 #   bench[=N][@ENV=V,...]       N bench lines (default 2), --steps 40 --warmup 5  -> bench_STEP_I.json
+#   benchw6[=N][@ENV=V,...]     the same for yolov7-w6 1280 bs 8                  -> benchw6_STEP_I.json
 #   dispatch[=NAME]             scripts/dump_dispatch.py (default dispatch of the 3 bench plans) -> dispatch_NAME.txt
 #   lib=NAME                    run the following steps on yolo-series_amd/yv7/libyv7_NAME.so (an
 #                               A/B baseline built elsewhere); lib=cur restores the tree's library
@@ -61,6 +62,13 @@ for step in "$@"; do
         env $(envof "$envs") timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --no-cpu-baseline \
           > $f 2> ${f%.json}.err || exit 1
         python -c "import json;d=json.load(open('$f'));print('bench', '$f', '$envs', d['value'], d['detail']['serial_forward_ms'])"
+      done ;;
+    benchw6)
+      for r in $(seq 1 ${arg:-2}); do
+        f=$O/benchw6_${n}_$r.json
+        env $(envof "$envs") timeout -k 10 300 python -u bench.py --model yolov7-w6 --batch 8 --img 1280 --steps 40 \
+          --warmup 5 --no-cpu-baseline > $f 2> ${f%.json}.err || exit 1
+        python -c "import json;d=json.load(open('$f'));print('benchw6', '$f', '$envs', d['value'], d['detail']['serial_forward_ms'])"
       done ;;
     dispatch)
       timeout -k 10 300 python -u scripts/dump_dispatch.py $O/dispatch_${arg:-cur}.txt > $O/dispatch_${arg:-cur}.log 2>&1 \

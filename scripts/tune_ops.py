@@ -18,7 +18,7 @@ import torch  # noqa: E402
 
 from models.yolo import Model  # noqa: E402
 from yv7 import _lib as L  # noqa: E402
-from yv7.runtime import Plan  # noqa: E402
+from yv7.runtime import Plan, kernel_key  # noqa: E402
 from yv7.synthetic import synthetic_state_dict  # noqa: E402
 
 RING = [100 + 10 * c + s for c in range(6) for s in (0, 2, 4)]
@@ -77,14 +77,18 @@ for i in convs:
                 continue
             t[v].append(a_)
             tot[v].append(b_)
-    plan.set_op_variant(i, 0)
     med = {v: statistics.median(ts) for v, ts in t.items() if ts}
     totm = {v: statistics.median(ts) for v, ts in tot.items() if ts}
     best = min(med, key=med.get)
-    rows.append({'op': i, 'desc': desc, 'us': med, 'fwd_us': totm, 'best': best})
+    # the kernel the winner actually launches (a forced variant the shape does not support falls back
+    # to another kernel, which may be what won)
+    plan.set_op_variant(i, best)
+    kern = ','.join(kernel_key(k) for k in plan.op_kernels(B, H, H, torch.float16)[i])
+    plan.set_op_variant(i, 0)
+    rows.append({'op': i, 'desc': desc, 'us': med, 'fwd_us': totm, 'best': best, 'best_kernel': kern})
     print(f'{i:3d} {desc:28s} default {med[0]:7.1f}  best {best:4d} {med[best]:7.1f}  gain {med[0] - med[best]:6.1f}'
           f'   fwd {totm[0] / 1e3:.3f} -> {totm[best] / 1e3:.3f} ms   top3 '
-          + ' '.join(f'{v}:{med[v]:.1f}' for v in sorted(med, key=med.get)[:3]), flush=True)
+          + ' '.join(f'{v}:{med[v]:.1f}' for v in sorted(med, key=med.get)[:3]) + f'   [{kern}]', flush=True)
 print(f'sum of per-op gains: {sum(r["us"][0] - r["us"][r["best"]] for r in rows):.1f} us')
 if a.out:
     with open(a.out, 'w') as f:

@@ -12,7 +12,7 @@ and 239: N-split), the column-group 3x3 halo ring (262), the
 low-resolution 3x3 kernel (270-273: 80 / 64-pixel tiles of 4 images x 4 columns, 128 / 64 channels;
 274 / 277-279: stride 2; 275 / 276: 160-pixel tiles), the register-weight 3x3 kernel (280-284: stride 2,
 285-288: stride 1; cin 64 / 128, 2-5 ring slots, 2-8-row tiles, with and without the stagger), the register-weight 1x1 kernel (290-295: cin 128 / 256 / 512, with and
-without the stagger) and
+without the stagger; 302 / 303: cin 256 with 128-channel N slices) and
 the alternative Detect heads (92, 97, and 99: the 64 x 256 ring that was the default before the
 persistent head).  A variant a layer's shape
 does not support falls back to the tuned kernel, which the check then covers again.
@@ -32,7 +32,7 @@ CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15, 17,
                  100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
                  201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274, 275, 276,
                  277, 278, 279, 280, 281, 282, 283, 284, 285, 286, 287, 288, 290, 291, 292, 293,
-                 294, 295]
+                 294, 295, 302, 303]
 DET_VARIANTS = [92, 97, 99]
 
 
@@ -88,7 +88,7 @@ RAGGED = {'nc': 3, 'depth_multiple': 1.0, 'width_multiple': 1.0,
 
 @pytest.mark.parametrize('B', [5, 6])
 def test_fragment_kernels_ragged(B):
-    """The fragment kernels (conv_lr.hip 270-279, conv_s2.hip 280-288, conv_w1.hip 290-295) on partial
+    """The fragment kernels (conv_lr.hip 270-279, conv_s2.hip 280-288, conv_w1.hip 290-295, 302-303) on partial
     trailing image groups / pixel tiles and half-masked channel pairs, op by op against fp32 torch."""
     import copy
     from models.yolo import Model
@@ -102,7 +102,7 @@ def test_fragment_kernels_ragged(B):
     convs = [i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV]
     lines = []
     for v in [0, 270, 271, 272, 273, 274, 275, 276, 277, 278, 279, 280, 281, 282, 283, 284, 285, 286, 287, 288,
-              290, 291, 292, 293, 294, 295]:
+              290, 291, 292, 293, 294, 295, 302, 303]:
         for i in convs:
             plan.set_op_variant(i, v)
         z, xs = plan.forward(x)
@@ -122,7 +122,7 @@ def test_variant_api_rejects_hooks():
     plan = m.plan()
     conv = next(i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV)
     for v in (12, 13, 14, 16, 18, 19, 90, 91, 93, 94, 298, 160, 105, 211, 221, 233, 237, 238, 240, 241,
-              248, 255, 259, 260, 261, 263, 289, 296, 911):
+              248, 255, 259, 260, 261, 263, 289, 296, 304, 911):
         with pytest.raises(RuntimeError):
             plan.set_op_variant(conv, v)
     with pytest.raises(RuntimeError):

@@ -2051,6 +2051,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // the register-weight 1x1 kernel (conv_w1.hip): 290 + configuration
   if (!det && variant >= 290 && variant <= 295 && w1_supported(p, variant - 290))
     return launch_conv_w1(p, variant - 290, device_cus(), st);
+  if (!det && variant >= 302 && variant <= 303 && w1_supported(p, variant - 296))   // its rows 6-7
+    return launch_conv_w1(p, variant - 296, device_cus(), st);
   if (!det && variant >= 299 && variant <= 301 && w1_supported(p, 1)) return launch_conv_w1(p, 1, device_cus(), st);   // its hooks
   // The register-weight 3x3 kernel (conv_s2.hip) at stride 1, checked before the low-resolution rule
   // below (which would take the 204 800-pixel layers).  In-network, one layer forced at a time
@@ -2077,7 +2079,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // (640) are equal either way.  YV7_LR=0: off.
   static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
   if (!det && variant == 0 && lr && (long)p.M <= 204800 && p.k == 3 && p.s == 1 &&
-      !((long)p.B * (p.H / 16) * (p.W / 16) >= 2048 && ws64_supported(p))) {
+      !((long)p.B * (p.H / 16) * (p.W / 16) >= 800 && ws64_supported(p))) {
     const bool t5 = p.H % 5 == 0;
     const long t128 = (long)((p.B + 3) / 4) * (p.H / (t5 ? 5 : 4)) * (p.W / 4) * (p.cout / 128);
     int cfg = (p.cout % 128 == 0 && t128 >= 400 ? 0 : 1) + (t5 ? 0 : 2);
@@ -2089,8 +2091,12 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (p.H % 10 == 0) {
       const long g10 = (long)((p.B + 3) / 4) * (p.H / 10) * (p.W / 4);
       if (p.cout % 128 == 0 && p.cout >= 2 * p.cin && p.cin <= 384 && g10 * (p.cout / 128) >= 400) cfg = 5;
-      else if (p.cout != 128 && p.cout % 64 == 0 && g10 * (p.cout / 64) >= 640) cfg = 6;
+      else if (p.cout != 128 && p.cout % 64 == 0 && g10 * (p.cout / 64) >= 480) cfg = 6;
     }
+    // Round 5 (profiles/r5_misc/tune_small_w6.txt, us): 160 x 64 from 480 such tiles (w6 bs 8 384->384 @40
+    // 38.0 / 37.9 / 37.1 / 37.3 -> 35.6-35.9); 64-pixel tiles on the 3 200-pixel layers (w6 bs 8 @20:
+    // 512->512 25.3 / 25.0 / 25.2 -> 23.7-24.1, 512->256 18.4 -> 17.1, 256->256 11.3 -> 10.4)
+    if (cfg == 1 && p.M <= 6400 && lr_supported(p, 3)) cfg = 3;
     if (lr_supported(p, cfg)) return launch_conv_lr(p, cfg, st);
   }
   // 3x3 stride-2 layers with 64 / 128 input channels and at least 204 800 output pixels: the register-weight
@@ -2108,13 +2114,14 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // network, one layer forced at a time (scripts/tune_ops.py, profiles/r5_w1/tune_*.txt, us, dispatch ->
   // w1): yolov7 bs 32 128->128 @160 87.5 -> 75.2 (cfg 0), 256->256 @160 187.5 -> 163.5, @80 58.3 -> 49.1
   // (cfg 3), 512->512 @80 147.5 -> 119.9, @40 47.6 -> 39.6 (cfg 5), 512->384 @80 131.1 -> 113.1 (cfg 2);
-  // yolov7-w6 bs 8 128->128 @320 91.3 -> 73.3, 512->256 @160 90.7 -> 65.5.  Narrower grids keep the
-  // rings below.  YV7_W1=0: off.
+  // yolov7-w6 bs 8 128->128 @320 91.3 -> 73.3, 512->256 @160 90.7 -> 65.5; 256->128 with a 128-channel
+  // N slice (cfg 7; profiles/r5_misc/tune_small_w6.txt) @320 139.9 -> 123.6, @160 43.7 -> 34.1.  Narrower
+  // grids keep the rings below.  YV7_W1=0: off.
   static const int w1k = [] { const char* e = getenv("YV7_W1"); return e ? atoi(e) : 1; }();
   if (!det && variant == 0 && w1k && one && !p.pool) {
     int cfg = -1;
     if (p.cin == 128 && p.M >= 409600) cfg = 0;
-    else if (p.cin == 256 && p.M >= 204800) cfg = 3;
+    else if (p.cin == 256 && p.M >= 204800) cfg = p.cout == 128 ? 7 : 3;
     else if (p.cin == 512 && p.M >= 51200) cfg = p.cout % 256 == 0 ? 5 : (p.M >= 204800 ? 2 : -1);
     if (cfg >= 0 && w1_supported(p, cfg)) return launch_conv_w1(p, cfg, device_cus(), st);
   }
@@ -2227,10 +2234,12 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     if (variant == 232 && (one || p.cin % BKE == 0)) return launch_p8n(p, one, st);
   }
   if (!det && p.cout > 32) {
-    // 64 -> 64 3x3: the persistent weight-stationary kernel once every CU gets >= 8 tiles (scripts/
-    // convbench.hip, bs 32, same box: @320 423 -> 337 us, @160 95 -> 79 us vs the halo kernel; @80,
-    // 3 tiles per CU, its prologue does not amortise); 12-16 are its microbenchmark hooks
-    if (((variant == 0 && (long)p.B * (p.H / 16) * (p.W / 16) >= 2048) || (variant >= 11 && variant <= 19)) &&
+    // 64 -> 64 3x3: the persistent weight-stationary kernel from 800 tiles of 16 x 16 (scripts/
+    // convbench.hip, bs 32, same box: @320 423 -> 337 us, @160 95 -> 79 us vs the halo kernel).  Round 5:
+    // its 8-wave form also takes the 800-tile layers from conv_lr (one layer forced at a time,
+    // profiles/r5_misc/tune_small_*.txt, us: yolov7 bs 32 @80 27.3 / 26.2 / 26.8 -> 24.1 / 24.2 / 24.1,
+    // yolov7-w6 bs 8 @160 25.7 / 26.3 / 25.7 -> 24.1 / 24.5 / 24.5); 12-16 are its microbenchmark hooks
+    if (((variant == 0 && (long)p.B * (p.H / 16) * (p.W / 16) >= 800) || (variant >= 11 && variant <= 19)) &&
         ws64_supported(p))
       return launch_conv_ws64(p, st);
     if ((variant == 0 || variant == 10) && halo_supported(p)) return launch_conv_halo(p, st);

@@ -285,11 +285,13 @@ __global__ __launch_bounds__(512, 2) void conv1x1_rw_kernel(const ConvParams p, 
   vmwait<0>();
 }
 
-// configurations (variants 290 + row): {NCH, TN, TPF, PG, NG, NS, STG, IC}.  0-2: an interval per 64-
-// channel chunk (cin 128 / 256 / 512), no stagger; 3-5: an interval per tile, stagger 1.
+// configurations (variants 290 + row for rows 0-5, 296 + row for rows 6-7): {NCH, TN, TPF, PG, NG, NS,
+// STG, IC}.  0-2: an interval per 64-channel chunk (cin 128 / 256 / 512), no stagger; 3-5: an interval per
+// tile, stagger 1; 6-7: cin 256 with a 128-channel N slice (cfg 3's is 256: half its waves would compute
+// masked channels of a 128-output layer).
 #define W1_CFGS(X)                                                                                             \
   X(0, 4, 8, 2, 8, 1, 4, 0, 1) X(1, 8, 4, 4, 2, 4, 8, 0, 1) X(2, 16, 2, 4, 2, 4, 8, 0, 1) X(3, 8, 4, 2, 2, 4, 4, 1, 4) \
-  X(4, 4, 8, 1, 8, 1, 4, 1, 2) X(5, 16, 2, 2, 1, 8, 4, 1, 8)
+  X(4, 4, 8, 1, 8, 1, 4, 1, 2) X(5, 16, 2, 2, 1, 8, 4, 1, 8) X(6, 8, 4, 1, 4, 2, 4, 1, 4) X(7, 8, 2, 2, 2, 4, 4, 1, 4)
 #define W1_ROW(i, nch, tn, tpf, pg, ng, ns, stg, ic) {nch, tn, tpf, pg, ng, ns, stg, ic},
 constexpr int W1_CFG[][8] = {W1_CFGS(W1_ROW)};
 constexpr int W1_NCFG = sizeof(W1_CFG) / sizeof(W1_CFG[0]);
