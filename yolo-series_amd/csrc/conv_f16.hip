@@ -85,6 +85,33 @@ struct KCursor {
   }
 };
 
+// Chunk-major K walk of a 3x3 (or 1x1 strided) implicit GEMM with cin % 64 == 0, for the 8-phase rings:
+// K step kt = (64-channel chunk cc, tap) with the tap fastest, so the nine taps of one chunk — which share
+// most of their 128-byte input lines (stride 2: each line serves ~2.25 taps; stride 1: ~9) — are staged
+// within nine consecutive K steps instead of one whole channel sweep apart (tap-major: 256 pixels x cin
+// between two taps of a line, more than an XCD's L2 holds with every block of the XCD doing the same;
+// round 5: 512->512 s2 @40 read its input 8.3 times from HBM / MALL, profiles/r5_pmc_ops.txt).  The
+// weights keep the tap-major [cout][k * k * cin] layout; the B offset follows the same (tap, cc).
+struct KWalk {
+  int cc, tap, rr, ss;
+  __device__ __forceinline__ void init() { cc = tap = rr = ss = 0; }
+  __device__ __forceinline__ void advance(const ConvParams& p) {
+    if (++tap == p.k * p.k) {
+      tap = rr = ss = 0;
+      ++cc;
+    } else if (++ss == p.k) {
+      ss = 0;
+      ++rr;
+    }
+  }
+  __device__ __forceinline__ uint32_t a_offset(const ConvParams& p) const {
+    return (uint32_t)(((rr * (p.W + 2 * BORDER) + ss) * p.xc + cc * BKE) * 2);
+  }
+  __device__ __forceinline__ uint32_t b_offset(const ConvParams& p) const {
+    return (uint32_t)((tap * p.cin + cc * BKE) * 2);
+  }
+};
+
 // A-operand source of one K step (BK deep) for RA rows: uniform case (1x1, or cin % BK == 0) = per-row
 // offset + scalar step offset; otherwise per-lane tap tracking (cin of 8..56: tiny's narrow layers).
 template <bool ONE, int RA, int BK = BKE>
@@ -1403,7 +1430,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   // ---- staging cursors (A and B halves are staged in different phases, each in K-tile order)
   int a_it = 0, a_kt = 0, b_it = 0, b_kt = 0, a_gk = 0, b_gk = 0;
   uint32_t a_off[2][AP], b_off[2][BP], a_so = 0;
-  KCursor<BKE> su;
+  KWalk sa, sb;   // (!ONE) the A and B halves' chunk-major K walks (staged in different phases)
   auto stage_a = [&](int h) {   // half h (0 / 1) of K-tile a_gk
     if (h == 0) {
       if (a_kt == 0) {
@@ -1414,10 +1441,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
           if (q) pw.advance(p, 64);
           a_off[q / AP][q % AP] = a_origin(p, pw.b, pw.ho, pw.wo, c);
         }
-        su.init(p, a_kt * BKE);
+        sa.init();
       }
-      a_so = ONE ? (uint32_t)a_kt * BKE * 2 : su.offset(p);
-      if (!ONE) su.advance(p);
+      a_so = ONE ? (uint32_t)a_kt * BKE * 2 : sa.a_offset(p);
+      if (!ONE) sa.advance(p);
     }
     unsigned char* d = smem + (a_gk & 1) * BUF + h * AHB;
 #pragma unroll
@@ -1427,17 +1454,23 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       if (++a_kt == nk) { a_kt = 0; ++a_it; }
     }
   };
+  uint32_t b_so = 0;
   auto stage_b = [&](int h) {   // half h of K-tile b_gk; staged B1 first, then B0
-    if (h == 1 && b_kt == 0) {
-      const int n0 = tile_at(b_it) % nN * BN;
+    if (h == 1) {
+      if (b_kt == 0) {
+        const int n0 = tile_at(b_it) % nN * BN;
 #pragma unroll
-      for (int q = 0; q < 2 * BP; ++q)
-        b_off[q / BP][q % BP] =
-            (uint32_t)(((n0 + (q / BP) * BHR + ((q % BP) * 8 + wave) * 8 + lr) * p.kpad + c * 8) * 2);
+        for (int q = 0; q < 2 * BP; ++q)
+          b_off[q / BP][q % BP] =
+              (uint32_t)(((n0 + (q / BP) * BHR + ((q % BP) * 8 + wave) * 8 + lr) * p.kpad + c * 8) * 2);
+        sb.init();
+      }
+      b_so = ONE ? (uint32_t)b_kt * BKE * 2 : sb.b_offset(p);
+      if (!ONE) sb.advance(p);
     }
     unsigned char* d = smem + (b_gk & 1) * BUF + 2 * AHB + h * BHB;
 #pragma unroll
-    for (int j = 0; j < BP; ++j) dma16(wr, d + (j * 8 + wave) * 8 * ROWB, b_off[h][j], (uint32_t)b_kt * BKE * 2);
+    for (int j = 0; j < BP; ++j) dma16(wr, d + (j * 8 + wave) * 8 * ROWB, b_off[h][j], b_so);
     if (h == 0) {
       ++b_gk;
       if (++b_kt == nk) { b_kt = 0; ++b_it; }
@@ -1619,10 +1652,13 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
 
   const int nN = (p.cout + BN - 1) / BN;
   const int T = ((p.M + BM - 1) / BM) * nN;
-  const int G = gridDim.x;
   const int nk = p.kpad / BKE;
-  const int ntl = (T - (int)blockIdx.x + G - 1) / G;
+  // XCD-major tile order (round 5): the nN tiles of one pixel block run on one XCD and share its input
+  // rows in that L2 (round robin put them on nN different XCDs)
+  const TileWalk tw = xcd_tile_walk(T);
+  const int ntl = tw.count();
   const int total = ntl * nk;
+  if (total == 0) return;
 
   const auto xr = make_rsrc(p.x, p.xbytes);
   const auto wr = make_rsrc(p.w, p.wbytes);
@@ -1631,12 +1667,12 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
 
   // ---- staging cursor: K-tile s_gk, half h = A half h + B half h
   int s_it = 0, s_kt = 0, s_gk = 0;
-  uint32_t a_off[2][2], b_off[2], a_so = 0;
-  KCursor<BKE> su;
+  uint32_t a_off[2][2], b_off[2], a_so = 0, b_so = 0;
+  KWalk su;
   auto stage = [&](int h) {
     if (h == 0) {
       if (s_kt == 0) {
-        const int t = blockIdx.x + s_it * G;
+        const int t = tw.at(s_it);
         PixelWalk pw(p, (t / nN) * BM + wave * 8 + lr);
 #pragma unroll
         for (int q = 0; q < 4; ++q) {
@@ -1646,15 +1682,16 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
         const int n0 = t % nN * BN;
 #pragma unroll
         for (int q = 0; q < 2; ++q) b_off[q] = (uint32_t)(((n0 + q * 64 + wave * 8 + lr) * p.kpad + c * 8) * 2);
-        su.init(p, 0);
+        su.init();
       }
-      a_so = ONE ? (uint32_t)s_kt * BKE * 2 : su.offset(p);
+      a_so = ONE ? (uint32_t)s_kt * BKE * 2 : su.a_offset(p);
+      b_so = ONE ? (uint32_t)s_kt * BKE * 2 : su.b_offset(p);
       if (!ONE) su.advance(p);
     }
     unsigned char* d = smem + (s_gk % 3) * BUF;
 #pragma unroll
     for (int j = 0; j < 2; ++j) dma16(xr, d + h * AH + (j * 8 + wave) * 8 * ROWB, a_off[h][j], a_so);
-    dma16(wr, d + 2 * AH + h * BH + wave * 8 * ROWB, b_off[h], (uint32_t)s_kt * BKE * 2);
+    dma16(wr, d + 2 * AH + h * BH + wave * 8 * ROWB, b_off[h], b_so);
     if (h == 1) {
       ++s_gk;
       if (++s_kt == nk) { s_kt = 0; ++s_it; }
@@ -1664,7 +1701,7 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
   f4 acc[2][4][2];
   int cm0 = 0, cn0 = 0;
   auto init_tile = [&](int i) {
-    const int t = blockIdx.x + i * G;
+    const int t = tw.at(i);
     cm0 = (t / nN) * BM;
     cn0 = (t % nN) * BN;
 #pragma unroll
