@@ -613,7 +613,7 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     issue();
-    if constexpr (HOOK != 1) {
+    if constexpr (HOOK != 1 && HOOK != 3) {
       // staging: the sigmoid of every logit into zs (z's layout); the 4 box columns of each row are
       // decoded in det_tail_fixed (one (row, column) per thread there, beside the row scores)
       float* zs = reinterpret_cast<float*>(es);
@@ -633,7 +633,7 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
     const long long zb = (long long)mb * p.nrows + p.row_off + (m0 - mb * hw);
     const auto zr = make_rsrc(p.z + (size_t)zb * 85, 0x7fffffffu);
     const auto br = make_rsrc(p.best ? p.best + (size_t)zb * 4 : p.z, 0x7fffffffu);
-    det_tail_fixed<BM, NTH>(p, es, tid, zr, br, zb);
+    if constexpr (HOOK < 2) det_tail_fixed<BM, NTH>(p, es, tid, zr, br, zb);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -649,7 +649,12 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
   const long T = (p.M + 63) / 64;
   const long per = (T + cus - 1) / cus;
   const int grid = (int)((T + per - 1) / per);
+  // microbenchmark hooks (scripts/detbench.hip; the ABI never accepts them): 98 = no sigmoid staging,
+  // 96 = no tail (decode, row scores, z / record stores), 95 = neither (the GEMM, its ring and the
+  // epilogue barriers only)
   if (p.variant == 98) YV7_LAUNCH(conv_det_pring_kernel<1>, dim3(grid), dim3(512), 0, st, p);
+  else if (p.variant == 96) YV7_LAUNCH(conv_det_pring_kernel<2>, dim3(grid), dim3(512), 0, st, p);
+  else if (p.variant == 95) YV7_LAUNCH(conv_det_pring_kernel<3>, dim3(grid), dim3(512), 0, st, p);
   else YV7_LAUNCH(conv_det_pring_kernel<0>, dim3(grid), dim3(512), 0, st, p);
   return hipGetLastError();
 }
@@ -2314,7 +2319,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // Detect head: the persistent head (conv_det_pring_kernel) where it applies; 98 = its
     // microbenchmark hook (no staging), 99 = the 64 x 256 ring below (the round-2 default)
     static const int det_pring = [] { const char* e = getenv("YV7_DET_PRING"); return e ? atoi(e) : 1; }();
-    if (((variant == 0 && det_pring) || variant == 98) && det_pring_supported(p)) return launch_det_pring(p, device_cus(), st);
+    if (((variant == 0 && det_pring) || variant == 98 || variant == 96 || variant == 95) && det_pring_supported(p))
+      return launch_det_pring(p, device_cus(), st);
     // BN = 256 covers the na*no = 255 channels of a pixel
     // (scripts/detbench.hip, bs 32, row scores on: 64 x 256 ring, 2 blocks per CU so one block's
     // epilogue runs beside the other's main loop: 124 / 42 / 25 us at 80 / 40 / 20; 128 x 256 ring
