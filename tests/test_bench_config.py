@@ -177,6 +177,30 @@ def test_w6_config_fp16_every_op():
           f'(reference half() emulation {((ze - zr).abs() / sc)[..., :4].max():.3g})')
 
 
+def test_tiny_config_fp16_every_op(batch):
+    """yolov7-tiny 640 at batch 32 (`bench.py --model yolov7-tiny`, the tiny line in profiles/): its exact
+    dispatch — which differs from the small-frame one the forced-variant tests see (round 5: the 8-wave
+    weight-stationary 3x3 takes its 64->64 @80 layers from 800 tiles) — every op against a plain PyTorch
+    fp32 reference on its own input (tests/opcheck.py), plus the row records vs z.
+    Reference: cfg/deploy/yolov7-tiny.yaml; models/common.py:110-111; models/yolo.py:42-63."""
+    m = fresh_model('yolov7-tiny').to(DEV).half()
+    plan = m.plan()
+    x = batch.to(DEV).half()
+    N = plan.num_rows(H, W)
+    z1 = torch.empty((B, N, plan.no), dtype=torch.float32, device=DEV)
+    rb = torch.empty((B, N, 4), dtype=torch.float32, device=DEV)
+    plan.forward_into(x, z1, rowbest=rb)
+    z, xs = plan.forward(x)
+    torch.cuda.synchronize()
+    assert torch.equal(z, z1), 'raw-logit output changed z'
+    out = check_ops(plan, x, B, H, W, raw=xs, z=z)
+    print('\nyolov7-tiny 640 bs32 fp16: ' + kernel_summary(out))
+    obj = z[..., 4]
+    best, cls = (z[..., 5:] * obj[..., None]).max(-1)
+    assert torch.equal(rb[..., 0], obj) and torch.equal(rb[..., 1], best)
+    assert torch.equal(rb[..., 2].view(torch.int32), cls.to(torch.int32))
+
+
 def test_fp8_config_every_op(batch):
     """BASELINE configs[4]: the product fp8 plan at yolov7 640 batch 32 (bench.py --dtype fp8).  The fp16
     ops against plain PyTorch fp32 references (tests/opcheck.py), every fp8 op against the restatement of
