@@ -3,7 +3,9 @@
 // Conv.fuseforward (models/common.py:110-111) at cfg/deploy/yolov7.yaml:20 (64->128 @320), the MP
 // blocks' stride-2 convs (yolov7.yaml:33 128->128 @160, :108 128->128 @80 in the head) and
 // yolov7-w6.yaml's 128-input stride-2 convs (:29 P3 entry 128->256 @320, and its head's).
-// y = act(conv2d(x, W', b', s=2, pad=1)).
+// y = act(conv2d(x, W', b', s=2, pad=1)).  The same kernel with S = 1 (configurations 5-8) serves the
+// large 64- and 128-input stride-1 3x3 layers (yolov7.yaml:19 64->64 @320, the ELAN 3x3 128->128 @80 and
+// the head's RepConv 128->256 @80; the dispatch rule in conv_f16.hip launch_conv_f16).
 //
 // Why: the stride-2 layers were the furthest below their roofline (yolov7: 517 us
 // against a 174 us roof; 64->128 s2 @320 alone 190 us against 79).  Their implicit-GEMM rings stage one
