@@ -1949,44 +1949,6 @@ hipError_t launch_pring(const ConvParams& p, bool one, int occ, hipStream_t st) 
              : launch_pring_act<BM, BN, WM, WN, STAGES, false, BK>(p, grid, st);
 }
 
-// The 8-phase ring with its partial last round split off (round 5).  A 1x1 layer whose 256 x 256 tiles
-// fill R >= 2 rounds of the CUs with the last one under half full (yolov7 bs 32: 1024->1024 @40, 800
-// tiles = 3 rounds + 32 tiles; 1024->768 @40, 600 = 2 rounds + 88) runs the whole images that fit R - 1
-// rounds on the 8-phase ring and the remaining images — a pointer offset of whole bordered images — on
-// the 128 x 128 persistent ring, two blocks per CU (a quarter of the tile work each, so the tail takes
-// about a quarter of a round instead of a whole one).  The tail goes first: the op's last launch stays
-// the 8-phase ring (bench.py's kernel table files an op under its last kernel).  YV7_P8TAIL=0: off;
-// 2: the tail on the 256 x 128 8-phase ring instead.
-hipError_t launch_p8(const ConvParams& p, bool one, hipStream_t st);
-hipError_t launch_p8n(const ConvParams& p, bool one, hipStream_t st);
-hipError_t launch_p8_tail(const ConvParams& p, bool one, hipStream_t st) {
-  static const int mode = [] { const char* e = getenv("YV7_P8TAIL"); return e ? atoi(e) : 0; }();
-  const int cus = device_cus();
-  const long hw = (long)p.Ho * p.Wo;
-  const long nN = (p.cout + 255) / 256;
-  auto tiles = [&](long b) { return (b * hw + 255) / 256 * nN; };
-  const long T = tiles(p.B), R = (T + cus - 1) / cus;
-  if (!mode || !one || p.pool || R < 2 || T - (R - 1) * cus > cus / 2) return launch_p8(p, one, st);
-  int b1 = p.B - 1;
-  while (b1 > 0 && tiles(b1) > (R - 1) * cus) --b1;
-  if (b1 <= 0) return launch_p8(p, one, st);
-  const size_t xi = (size_t)(p.H + 2 * BORDER) * (p.W + 2 * BORDER) * p.xc * 2;
-  const size_t yi = (size_t)(p.Ho + 2 * BORDER) * (p.Wo + 2 * BORDER) * p.yc * 2;
-  if ((size_t)p.xbytes < (size_t)p.B * xi) return launch_p8(p, one, st);
-  ConvParams t = p;   // images b1 .. B - 1
-  t.B = p.B - b1;
-  t.M = (int)(t.B * hw);
-  t.x = static_cast<const unsigned char*>(p.x) + b1 * xi;
-  t.xbytes = (uint32_t)(p.xbytes - b1 * xi);
-  t.y = static_cast<unsigned char*>(p.y) + b1 * yi;
-  ConvParams a = p;   // images 0 .. b1 - 1
-  a.B = b1;
-  a.M = (int)(b1 * hw);
-  const hipError_t e = mode == 2 ? launch_p8n(t, one, st) : launch_pring<128, 128, 2, 2, 2>(t, one, 2, st);
-  if (e != hipSuccess) return e;
-  return launch_p8(a, one, st);
-}
-
 template <int BM, int BN, int WM, int WN, int STAGES, bool ONE, bool DET = false>
 hipError_t launch_ring(const ConvParams& p, hipStream_t st) {
   const int nM = (p.M + BM - 1) / BM, nN = (p.cout + BN - 1) / BN;
@@ -2268,7 +2230,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
       const long t2n = (long)((p.M + 255) / 256) * (p.cout / 128);
       if (t2n >= 150 && t2n <= 250) return launch_p8n(p, false, st);
     }
-    if (p8_default(p)) return launch_p8_tail(p, one, st);
+    if (p8_default(p)) return launch_p8(p, one, st);
     if (one) {
       // (a cout that is not a multiple of 256 — the tensor-fused pair 512->256+128 @80 — would leave
       // half of every last 256-wide N tile idle: the 128 x 128 ring below, 148.8 -> 124.2 us in-network,
