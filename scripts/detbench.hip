@@ -45,6 +45,13 @@ int main(int argc, char** argv) {
     p.xbytes = (uint32_t)(yv7::bordered_pixels(B, l.hw, l.hw) * l.cin * 2);
     p.wbytes = (uint32_t)(256 * l.cin * 2);
     p.z = z; p.nrows = nrows; p.row_off = row_off; p.na = na; p.no = no; p.stride = l.stride;
+    // the fragment-packed weight copy the plan makes for the register-weight head (conv_det_rw_kernel)
+    void* wf = nullptr;
+    const size_t wfb = yv7::frag_bytes(l.cin, 255, 1);
+    CK(hipMalloc(&wf, wfb));
+    CK(yv7::pack_frag(w, l.cin, l.cin, 255, 1, wf, 0));
+    CK(hipDeviceSynchronize());
+    p.wf = wf; p.wfbytes = (uint32_t)wfb;
     for (int a = 0; a < 6; ++a) p.anchor[a] = 10.f + a;
     for (int withbest = 0; withbest < 2; ++withbest) {
       p.best = withbest ? best : nullptr;

@@ -33,7 +33,7 @@ CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15, 17,
                  201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274, 275, 276,
                  277, 278, 279, 280, 281, 282, 283, 284, 285, 286, 287, 288, 290, 291, 292, 293,
                  294, 295, 302, 303]
-DET_VARIANTS = [92, 97, 99]
+DET_VARIANTS = [92, 94, 97, 99]
 
 
 @pytest.fixture(scope='module', autouse=True)

@@ -479,7 +479,7 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
   constexpr int BM = 64, BN = 256, WM = 2, WN = 4, NW = 8, NTH = 512;
   constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
   constexpr int RB = BN / 8 / NW;                  // 4 weight wave-instructions per stage (A: 1)
-  constexpr int PER = 1 + RB;
+  constexpr int PER = HOOK == 4 ? 1 : 1 + RB;   // (hook 4: no weight DMA)
   constexpr int STAGE = (BM + BN) * ROWB;          // 40 KiB
   constexpr int RING = 2 * STAGE;
   constexpr int LDS = RING + det_lds(BM, BN);
@@ -521,8 +521,10 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
     const bool live = i_it < ntl;
     const uint32_t so = (uint32_t)i_k * BKE * 2;
     dma16(xr, As + wave * 8 * ROWB, i_aoff, so);
+    if constexpr (HOOK != 4) {
 #pragma unroll
-    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * 8 * ROWB, live ? b_off[j] : OOB, so);
+      for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * 8 * ROWB, live ? b_off[j] : OOB, so);
+    }
     asm volatile("" ::: "memory");
     ++i_q;
     if (++i_k == nk) {
@@ -638,6 +640,167 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
+// Register-weight Detect head (round 5, the default for K = 256 / 512: yolov7's P3 / P4 heads, w6's P3
+// / P4).  scripts/detbench.hip's hook 93 (the persistent head above without its weight DMA,
+// profiles/r5_det/detbench_hooks_noweights.txt) runs 256->255 @80 bs 32 in 41-50 us against 91-92 and
+// 512->255 @40 in 20 against 40: restaging the 256-channel weight tile (4 of the 5 pieces of every K
+// step) for every 64-pixel tile costs as much as the whole rest of the kernel.  Here the weights never
+// move: wave w keeps channels 32 w .. 32 w + 31 for all of K in VGPRs (2 x NCH fragments from the
+// fragment-packed copy: 64 VGPRs at K = 256, 128 at K = 512), the ring stages only the tile's pixels (8
+// KiB per K step), and the wave computes those 32 channels for all 64 pixels (4 pixel fragments per read
+// step, each feeding 2 MFMAs).  Epilogue and row records as conv_det_pring_kernel (det_tail_fixed; the
+// same sigmoid and decode: bit-identical z and records).
+template <int NCH>
+__global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p) {
+  constexpr int BM = 64, BN = 256, NTH = 512, TM = 4, TN = 2, NK = NCH / 2;
+  constexpr int PER = 1;                           // one A piece per wave per stage
+  constexpr int STAGE = BM * ROWB;                 // 8 KiB
+  constexpr int RING = 2 * STAGE;
+  constexpr int LDS = RING + det_lds(BM, BN);
+  static_assert(LDS <= 160 * 1024, "LDS budget");
+  constexpr int NO = 85, NA = 3;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
+  unsigned char* es = smem + RING;                 // zs + row table
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, li = lane & 15;
+  const int T = (p.M + BM - 1) / BM;
+  const TileWalk tw = xcd_tile_walk(T);
+  const int ntl = tw.count();
+  if (ntl == 0) return;
+
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto wr = make_rsrc(p.wf, p.wfbytes);
+  // the wave's weights: fragment (16-channel group 2 wave + j, K step c) at ((2 wave + j) * NCH + c) KiB
+  u4 wreg[TN][NCH];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const uint32_t base = (uint32_t)(((2 * wave + j) * NCH) * 1024 + lane * 16);
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+      wreg[j][c] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(wr, base, (uint32_t)(c * 1024), 0));
+  }
+  const int lr = lane >> 3;
+  const int c8 = (lane & 7) ^ lr;
+  const int hw = p.Ho * p.Wo;
+  auto a_off = [&](int it) -> uint32_t {
+    if (it >= ntl) return OOB;
+    const int m = tw.at(it) * BM + wave * 8 + lr;
+    if (m >= p.M) return OOB;
+    const int b = m / hw, cell = m - b * hw, ho = cell / p.Wo, wo = cell - ho * p.Wo;
+    return (uint32_t)((pix_index(b, ho, wo, p.H, p.W) * p.xc + p.xoff + c8 * 8) * 2);
+  };
+  // stage q = (tile it, K step k) into slot q & 1
+  int i_it = 0, i_k = 0, i_q = 0;
+  uint32_t i_aoff = a_off(0);
+  auto issue = [&]() __attribute__((always_inline)) {
+    dma16(xr, smem + (i_q & 1) * STAGE + wave * 8 * ROWB, i_aoff, (uint32_t)i_k * BKE * 2);
+    asm volatile("" ::: "memory");
+    ++i_q;
+    if (++i_k == NK) {
+      i_k = 0;
+      ++i_it;
+      i_aoff = a_off(i_it);
+    }
+  };
+
+  f4 bv[TN];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wave * 32 + j * 16 + g * 4;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bv[j][e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
+  }
+  const int nst = p.best ? 10 : 8;   // epilogue stores per wave per tile (det_tail_fixed)
+  // z slot of each of this lane's 8 channels (the padding channel 255 -> a spare slot)
+  int zo[TN][4];
+#pragma unroll
+  for (int j = 0; j < TN; ++j)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int ch = wave * 32 + j * 16 + g * 4 + e;
+      const int ca = ch / NO;
+      zo[j][e] = ca < NA ? ca * BM * NO + (ch - ca * NO) : NA * BM * NO;
+    }
+  if (tid < 8) det_tab_ptrs<BM, BN>(es).anc[tid] = p.anchor[tid];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // weights, bias, anchors
+  issue();
+  issue();
+  for (int it = 0; it < ntl; ++it) {
+    const int m0 = tw.at(it) * BM;
+    f4 acc[TN][TM];
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int i = 0; i < TM; ++i) acc[j][i] = bv[j];
+#pragma unroll
+    for (int k = 0; k < NK; ++k) {
+      // stage (it, k) landed: younger are stage (it, 1) and the previous epilogue's stores at k = 0, the
+      // previous epilogue's stores at k = 1 (both stages of a tile start are issued before them)
+      if (k == 0) {
+        if (it > 0 && nst == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 10) : "memory");
+        else if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 8) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+      } else if (k == 1 && it > 0) {
+        if (nst == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      } else {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      }
+      __builtin_amdgcn_s_barrier();
+      if (k >= 1) issue();              // stage (it, k + 1) or the next tile's first stage
+      if (k == 0) det_table<BM, BN, NTH, false>(p, es, m0, tid);   // read after the K loop's last barrier
+      const unsigned char* As = smem + ((it * NK + k) & 1) * STAGE;
+#pragma unroll
+      for (int s2 = 0; s2 < 2; ++s2) {
+        const int ch = s2 * 4 + g;
+        u4 xa[TM];
+#pragma unroll
+        for (int i = 0; i < TM; ++i) {
+          const int row = i * 16 + li;
+          xa[i] = *reinterpret_cast<const u4*>(As + row * ROWB + swz(row, ch) * 16);
+        }
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int i = 0; i < TM; ++i)
+            acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wreg[j][2 * k + s2]),
+                                                               __builtin_bit_cast(h8, xa[i]), acc[j][i], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+      }
+    }
+    // epilogue: ring reads done -> the next tile's stage (it + 1, 1) into the free slot
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    issue();
+    // staging: the sigmoid of every logit into zs (z's layout); the box columns are decoded in
+    // det_tail_fixed
+    float* zs = reinterpret_cast<float*>(es);
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+      const int roff = (i * 16 + li) * NO;
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) zs[zo[j][e] + (zo[j][e] < NA * BM * NO ? roff : 0)] = det_sig(acc[j][i][e]);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    const int mb = m0 / hw;
+    const long long zb = (long long)mb * p.nrows + p.row_off + (m0 - mb * hw);
+    const auto zr = make_rsrc(p.z + (size_t)zb * 85, 0x7fffffffu);
+    const auto br = make_rsrc(p.best ? p.best + (size_t)zb * 4 : p.z, 0x7fffffffu);
+    det_tail_fixed<BM, NTH>(p, es, tid, zr, br, zb);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+bool det_rw_supported(const ConvParams& p) {
+  return p.wf && (p.kpad == 256 || p.kpad == 512) && p.wfbytes >= (uint32_t)(256 * p.kpad * 2);
+}
+
 bool det_pring_supported(const ConvParams& p) {
   const int hw = p.Ho * p.Wo;
   return p.k == 1 && p.s == 1 && p.na == 3 && p.no == 85 && p.cout == 255 && p.raw == nullptr &&
@@ -652,9 +815,18 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
   // microbenchmark hooks (scripts/detbench.hip; the ABI never accepts them): 98 = no sigmoid staging,
   // 96 = no tail (decode, row scores, z / record stores), 95 = neither (the GEMM, its ring and the
   // epilogue barriers only)
+  // the register-weight head (conv_det_rw_kernel) by default where the plan packed its weights (K = 256 /
+  // 512); 94 = the persistent head with staged weights, kept as a forced variant.  YV7_DET_RW=0: off.
+  static const int rw = [] { const char* e = getenv("YV7_DET_RW"); return e ? atoi(e) : 1; }();
+  if (rw && p.variant == 0 && det_rw_supported(p) && (p.kpad == 256 || rw == 2)) {   // (K = 512: 29 VGPRs spill)
+    if (p.kpad == 256) YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
+    else YV7_LAUNCH(conv_det_rw_kernel<16>, dim3(grid), dim3(512), 0, st, p);
+    return hipGetLastError();
+  }
   if (p.variant == 98) YV7_LAUNCH(conv_det_pring_kernel<1>, dim3(grid), dim3(512), 0, st, p);
   else if (p.variant == 96) YV7_LAUNCH(conv_det_pring_kernel<2>, dim3(grid), dim3(512), 0, st, p);
   else if (p.variant == 95) YV7_LAUNCH(conv_det_pring_kernel<3>, dim3(grid), dim3(512), 0, st, p);
+  else if (p.variant == 93) YV7_LAUNCH(conv_det_pring_kernel<4>, dim3(grid), dim3(512), 0, st, p);   // no weight DMA
   else YV7_LAUNCH(conv_det_pring_kernel<0>, dim3(grid), dim3(512), 0, st, p);
   return hipGetLastError();
 }
@@ -2319,7 +2491,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // Detect head: the persistent head (conv_det_pring_kernel) where it applies; 98 = its
     // microbenchmark hook (no staging), 99 = the 64 x 256 ring below (the round-2 default)
     static const int det_pring = [] { const char* e = getenv("YV7_DET_PRING"); return e ? atoi(e) : 1; }();
-    if (((variant == 0 && det_pring) || variant == 98 || variant == 96 || variant == 95) && det_pring_supported(p))
+    if (((variant == 0 && det_pring) || variant == 94 || variant == 98 || variant == 96 || variant == 95 ||
+         variant == 93) && det_pring_supported(p))
       return launch_det_pring(p, device_cus(), st);
     // BN = 256 covers the na*no = 255 channels of a pixel
     // (scripts/detbench.hip, bs 32, row scores on: 64 x 256 ring, 2 blocks per CU so one block's

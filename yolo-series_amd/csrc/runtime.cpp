@@ -122,6 +122,9 @@ bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7
 bool wants_frag(int dtype, const yv7_op_desc& o) {
   static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
   const int nch = o.cin / 32;
+  // the Detect head conv with K = 256 / 512 (conv_det_rw_kernel: the weights resident in VGPRs)
+  if (dtype == YV7_DT_F16 && o.kind == YV7_OP_DETECT)
+    return lr && o.k == 1 && (o.cin == 256 || o.cin == 512) && o.cout <= 256;
   if (!lr || dtype != YV7_DT_F16 || o.kind != YV7_OP_CONV || is_f8(o) || o.pool || o.cout % 16 || o.cout > 1024)
     return false;
   if (o.k == 1)   // conv_w1.hip: 1x1 stride 1 with 128 / 256 / 512 inputs
@@ -414,7 +417,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (v == 0) return true;
   const int kind = o.kind;
   if (is_f8(o)) return v == 81 || v == 82;   // fp8 1x1: staged quantize pass / fused quantization
-  if (kind == YV7_OP_DETECT) return v == 92 || v == 97 || v == 99;
+  if (kind == YV7_OP_DETECT) return v == 92 || v == 94 || v == 97 || v == 99;
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15 || v == 17) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
   return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
