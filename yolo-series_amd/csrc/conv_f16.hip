@@ -305,19 +305,24 @@ __device__ __forceinline__ void det_epilogue(const ConvParams& p, unsigned char*
 // its class, from the same sigmoid values z receives.  Four lanes per row, each over the classes
 // c = part, part + 4, ... (first maximum per lane), merged by shuffles: the larger score wins, an
 // equal score goes to the smaller class — the first maximum (general.py:683-684).
-template <int NC>
+// (NB: the lane's classes are loaded in NB batches — 2 under register pressure — and scanned in order.)
+template <int NC, int NB = 1>
 __device__ __forceinline__ void det_best_lane(const float* sg, int nc, int part, float& best, int& bc) {
   const float obj = sg[4];
   best = -1.0f;
   bc = 0x7fffffff;
   if constexpr (NC > 0) {
-    float v[NC / 4];
+    constexpr int NV = NC / 4 / NB;
 #pragma unroll
-    for (int i = 0; i < NC / 4; ++i) v[i] = sg[5 + part + 4 * i];
+    for (int b = 0; b < NB; ++b) {
+      float v[NV];
 #pragma unroll
-    for (int i = 0; i < NC / 4; ++i) {
-      const float s = v[i] * obj;
-      if (s > best) { best = s; bc = part + 4 * i; }
+      for (int i = 0; i < NV; ++i) v[i] = sg[5 + part + 4 * (b * NV + i)];
+#pragma unroll
+      for (int i = 0; i < NV; ++i) {
+        const float s = v[i] * obj;
+        if (s > best) { best = s; bc = part + 4 * (b * NV + i); }
+      }
     }
   } else if (nc > 1) {
     for (int c = part; c < nc; c += 4) {
@@ -411,7 +416,8 @@ __device__ __forceinline__ void det_tail(const ConvParams& p, unsigned char* sme
 //    the buffer range, where the store is dropped), so the epilogue's stores stay in flight behind
 //    counted vmcnt waits — they drain under the next tile's K loop and epilogue instead of stalling it.
 // Same arithmetic as det_stage / det_tail (bit-identical z and records).
-template <int BM, int NTH>
+// ZU: the z-store loop's unroll (2 under register pressure: the register-weight head at K = 512)
+template <int BM, int NTH, int ZU = 0>
 __device__ __forceinline__ void det_tail_fixed(const ConvParams& p, unsigned char* smem, int tid,
                                                __amdgpu_buffer_rsrc_t zr, __amdgpu_buffer_rsrc_t br, long long zb) {
   constexpr int NO = 85, NA = 3, BN = 256;
@@ -439,7 +445,7 @@ __device__ __forceinline__ void det_tail_fixed(const ConvParams& p, unsigned cha
       const float* sg = zs + (live ? r : 0) * NO;
       float best;
       int bc;
-      det_best_lane<80>(sg, NO - 5, part, best, bc);
+      det_best_lane<80, ZU ? 2 : 1>(sg, NO - 5, part, best, bc);
 #pragma unroll
       for (int d = 1; d < 4; d <<= 1) {
         const float ob = __shfl_xor(best, d, 64);
@@ -461,7 +467,8 @@ __device__ __forceinline__ void det_tail_fixed(const ConvParams& p, unsigned cha
   constexpr int GPP = NTH / NO;        // groups in flight per pass
   constexpr int IT = (NA * G + GPP - 1) / GPP;
   const int c = tid % NO, gg = tid / NO;
-#pragma unroll
+  constexpr int ZUN = ZU ? ZU : IT;
+#pragma unroll ZUN
   for (int k = 0; k < IT; ++k) {
     const int idx = gg + GPP * k;
     const bool valid = gg < GPP && idx < NA * G;
@@ -792,7 +799,7 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
     const long long zb = (long long)mb * p.nrows + p.row_off + (m0 - mb * hw);
     const auto zr = make_rsrc(p.z + (size_t)zb * 85, 0x7fffffffu);
     const auto br = make_rsrc(p.best ? p.best + (size_t)zb * 4 : p.z, 0x7fffffffu);
-    det_tail_fixed<BM, NTH>(p, es, tid, zr, br, zb);
+    det_tail_fixed<BM, NTH, NCH == 8 ? 0 : 2>(p, es, tid, zr, br, zb);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
@@ -818,7 +825,7 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
   // the register-weight head (conv_det_rw_kernel) by default where the plan packed its weights (K = 256 /
   // 512); 94 = the persistent head with staged weights, kept as a forced variant.  YV7_DET_RW=0: off.
   static const int rw = [] { const char* e = getenv("YV7_DET_RW"); return e ? atoi(e) : 1; }();
-  if (rw && p.variant == 0 && det_rw_supported(p) && (p.kpad == 256 || rw == 2)) {   // (K = 512: 29 VGPRs spill)
+  if (rw && p.variant == 0 && det_rw_supported(p) && (p.kpad == 256 || rw == 2)) {
     if (p.kpad == 256) YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
     else YV7_LAUNCH(conv_det_rw_kernel<16>, dim3(grid), dim3(512), 0, st, p);
     return hipGetLastError();
