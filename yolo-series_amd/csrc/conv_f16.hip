@@ -824,8 +824,10 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
   // epilogue barriers only)
   // the register-weight head (conv_det_rw_kernel) by default where the plan packed its weights (K = 256 /
   // 512); 94 = the persistent head with staged weights, kept as a forced variant.  YV7_DET_RW=0: off.
+  // In-network A/B, same box (profiles/r5_det/rw/, rw512/): 256->255 @80 82.7 -> 67.3 us, 512->255 @40
+  // 38.9 -> 35.6 us.
   static const int rw = [] { const char* e = getenv("YV7_DET_RW"); return e ? atoi(e) : 1; }();
-  if (rw && p.variant == 0 && det_rw_supported(p) && (p.kpad == 256 || rw == 2)) {
+  if (rw && p.variant == 0 && det_rw_supported(p)) {
     if (p.kpad == 256) YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
     else YV7_LAUNCH(conv_det_rw_kernel<16>, dim3(grid), dim3(512), 0, st, p);
     return hipGetLastError();
