@@ -657,10 +657,11 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
 // KiB per K step), and the wave computes those 32 channels for all 64 pixels (4 pixel fragments per read
 // step, each feeding 2 MFMAs).  Epilogue and row records as conv_det_pring_kernel (det_tail_fixed; the
 // same sigmoid and decode: bit-identical z and records).
-template <int NCH>
+// HOOK (detbench only, variant 91; the ABI never accepts it): 1 = no pixel DMA (stale LDS operands)
+template <int NCH, int HOOK = 0>
 __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p) {
   constexpr int BM = 64, BN = 256, NTH = 512, TM = 4, TN = 2, NK = NCH / 2;
-  constexpr int PER = 1;                           // one A piece per wave per stage
+  constexpr int PER = HOOK == 1 ? 0 : 1;           // one A piece per wave per stage
   constexpr int STAGE = BM * ROWB;                 // 8 KiB
   constexpr int RING = 2 * STAGE;
   constexpr int LDS = RING + det_lds(BM, BN);
@@ -702,7 +703,7 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
   int i_it = 0, i_k = 0, i_q = 0;
   uint32_t i_aoff = a_off(0);
   auto issue = [&]() __attribute__((always_inline)) {
-    dma16(xr, smem + (i_q & 1) * STAGE + wave * 8 * ROWB, i_aoff, (uint32_t)i_k * BKE * 2);
+    if constexpr (HOOK != 1) dma16(xr, smem + (i_q & 1) * STAGE + wave * 8 * ROWB, i_aoff, (uint32_t)i_k * BKE * 2);
     asm volatile("" ::: "memory");
     ++i_q;
     if (++i_k == NK) {
@@ -827,7 +828,12 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
   // In-network A/B, same box (profiles/r5_det/rw/, rw512/): 256->255 @80 82.7 -> 67.3 us, 512->255 @40
   // 38.9 -> 35.6 us.
   static const int rw = [] { const char* e = getenv("YV7_DET_RW"); return e ? atoi(e) : 1; }();
-  if (rw && p.variant == 0 && det_rw_supported(p)) {
+  if (rw && (p.variant == 0 || p.variant == 91) && det_rw_supported(p)) {
+    if (p.variant == 91) {   // its hook (no pixel DMA)
+      if (p.kpad == 256) YV7_LAUNCH((conv_det_rw_kernel<8, 1>), dim3(grid), dim3(512), 0, st, p);
+      else YV7_LAUNCH((conv_det_rw_kernel<16, 1>), dim3(grid), dim3(512), 0, st, p);
+      return hipGetLastError();
+    }
     if (p.kpad == 256) YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
     else YV7_LAUNCH(conv_det_rw_kernel<16>, dim3(grid), dim3(512), 0, st, p);
     return hipGetLastError();
@@ -2501,7 +2507,7 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     // microbenchmark hook (no staging), 99 = the 64 x 256 ring below (the round-2 default)
     static const int det_pring = [] { const char* e = getenv("YV7_DET_PRING"); return e ? atoi(e) : 1; }();
     if (((variant == 0 && det_pring) || variant == 94 || variant == 98 || variant == 96 || variant == 95 ||
-         variant == 93) && det_pring_supported(p))
+         variant == 93 || variant == 91) && det_pring_supported(p))
       return launch_det_pring(p, device_cus(), st);
     // BN = 256 covers the na*no = 255 channels of a pixel
     // (scripts/detbench.hip, bs 32, row scores on: 64 x 256 ring, 2 blocks per CU so one block's
