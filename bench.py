@@ -100,13 +100,14 @@ def launch_ranks(a, argv):
 def plumbing(a):
     """The N > 1 data path on CPU ranks (gloo): the same yv7.dist calls the GPU ranks make, minus the
     kernels.  Prints one JSON line with the world size the process group saw."""
-    dist.init_process_group('gloo')
+    from yv7 import dist as ydist
+    ydist.init('gloo')
     world, rank = dist.get_world_size(), dist.get_rank()
     if world != a.gpus:
         raise SystemExit(f'--gpus {a.gpus} but the process group has {world} ranks')
+    wd = ydist.Watchdog(rank)
     from models.yolo import Model
     from yv7 import _lib as L
-    from yv7 import dist as ydist
     from yv7.graph import compile_model
     from yv7.synthetic import synthetic_state_dict
     import contextlib
@@ -147,9 +148,12 @@ def plumbing(a):
     dist.all_reduce(flags, op=dist.ReduceOp.MIN)
     # the fields the GPU run reports per rank (here on gloo): the all-gather's time per batch and the
     # world size each rank's process group saw; plus each rank's shard of the global batch
+    wd.beat('plumbing all-gathers')
     t0 = time.perf_counter()
-    for _ in range(10):
-        ydist.gather_detections(det, src, cnt)
+    for i in range(10):
+        wd.beat(batch=i)
+        ydist.fault_point(rank, i)
+        ydist.guarded(lambda: ydist.gather_detections(det, src, cnt), 'detection all-gather', i)
     us = (time.perf_counter() - t0) / 10 * 1e6
     per = torch.tensor([us, float(dist.get_world_size()), float(lo), float(hi), float(in_order)], dtype=torch.float64)
     pl = [torch.zeros_like(per) for _ in range(world)]
@@ -164,6 +168,7 @@ def plumbing(a):
                           'allgather_us_per_batch': [round(float(v[0]), 1) for v in pl],
                           'per_rank_world_size_seen': [int(v[1]) for v in pl]}), flush=True)
     dist.barrier()
+    wd.stop()
     dist.destroy_process_group()
 
 
@@ -279,15 +284,23 @@ def main(argv=None):
     force_dist = os.environ.get('YV7_BENCH_DIST') == '1'
     distributed = world > 1 or force_dist
     torch.cuda.set_device(local)
+    from yv7 import dist as ydist
+    wd = None
     if distributed:
-        dist.init_process_group('nccl', device_id=torch.device(f'cuda:{local}'))
+        # process-group timeout + a host-side progress watchdog: a dead or hung peer ends this rank with a
+        # non-zero exit naming the rank, phase and batch, not a wait for the outer kill
+        ydist.init('nccl', torch.device(f'cuda:{local}'))
         if dist.get_world_size() != a.gpus:
             raise SystemExit(f'--gpus {a.gpus} but RCCL sees {dist.get_world_size()} ranks')
+        wd = ydist.Watchdog(rank)
     dev = torch.device(f'cuda:{local}')
+
+    def beat(phase=None, batch=None):
+        if wd is not None:
+            wd.beat(phase, batch)
 
     from models.yolo import Model
     from utils.general import nms_batched
-    from yv7 import dist as ydist
     from yv7.runtime import Plan
     from yv7.synthetic import synthetic_state_dict
 
@@ -334,7 +347,8 @@ def main(argv=None):
     if nstreams > 1:   # yv7.runtime.Inflight: the library's serving schedule, S batches in flight
         from yv7.runtime import Inflight
         prios = [int(v) for v in a.prio.split(',')] if a.prio else None
-        gather = (lambda d, s_, c: ydist.gather_detections(d, s_, c, force=force_dist)) if distributed else None
+        gather = (lambda d, s_, c: ydist.guarded(lambda: ydist.gather_detections(d, s_, c, force=force_dist),
+                                                 'detection all-gather', nstep[0] - 1)) if distributed else None
         runner = Inflight(plan, B, H, W, streams=nstreams, post=gather,
                           priorities=prios)
     zs = [torch.empty((B, N, plan.no), dtype=torch.float32, device=dev) for _ in range(nbuf)]
@@ -370,11 +384,15 @@ def main(argv=None):
     def post(k):
         nms_batched(zs[k], 0.25, 0.45, out=(dets[k], srcs[k], cnts[k]), rowbest=rowbests[k])
         if distributed:
-            ydist.gather_detections(dets[k], srcs[k], cnts[k], force=force_dist)
+            ydist.guarded(lambda: ydist.gather_detections(dets[k], srcs[k], cnts[k], force=force_dist),
+                          'detection all-gather', nstep[0] - 1)
 
     def step():
         k = nstep[0] % nbuf
         xk = xin[nstep[0] % len(xin)]
+        if distributed:
+            ydist.fault_point(rank, nstep[0])
+            beat('batches', nstep[0])
         nstep[0] += 1
         if runner is not None:
             if h2d is None:
@@ -405,6 +423,7 @@ def main(argv=None):
             post(k)
         nms_done[k].record(nms_stream)
 
+    beat('warmup')
     for _ in range(a.warmup):
         step()
     torch.cuda.synchronize()
@@ -445,6 +464,7 @@ def main(argv=None):
     if distributed:
         dist.barrier()
     elapsed = time.perf_counter() - t0
+    beat('after the timed region')
     rank_elapsed = [elapsed]
     if distributed:   # every rank's own time (per-rank img/s), then the job's: the slowest rank
         t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
@@ -677,9 +697,28 @@ def main(argv=None):
                 res['map50_parity'] = res['cpu_baseline']['map_parity']['map50']
         print(json.dumps(res), flush=True)
     if distributed:
+        beat('final barrier')
         dist.barrier()
+        wd.stop()
         dist.destroy_process_group()
 
 
+def run_rank(argv=None):
+    """main() for one rank.  In a multi-rank job an exception (e.g. a failed collective, re-raised by
+    yv7.dist.guarded with rank and batch) ends the process at once with exit code 1 after its traceback:
+    the interpreter's normal shutdown would tear down a process group whose peers may be gone."""
+    try:
+        main(argv)
+    except SystemExit:
+        raise
+    except BaseException:
+        if dist.is_initialized() and dist.get_world_size() > 1:
+            import traceback
+            traceback.print_exc()
+            sys.stderr.flush()
+            os._exit(1)
+        raise
+
+
 if __name__ == '__main__':
-    main()
+    run_rank()

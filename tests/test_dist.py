@@ -272,6 +272,70 @@ def test_bench_launcher_starts_ranks():
     assert r['per_rank_world_size_seen'] == [2, 2] and len(r['allgather_us_per_batch']) == 2
 
 
+def _start_ranks(world, extra_env, args):
+    """`world` bench.py ranks started directly (no torch.distributed.run, whose agent would tear the
+    survivors down itself): each rank's own failure handling is what the test sees."""
+    import subprocess
+    import sys
+    from bench import _free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    port = str(_free_port())
+    procs = []
+    for r in range(world):
+        env = {k: v for k, v in os.environ.items() if k not in ('YV7_DIST_FAULT',)}
+        env.update(extra_env, WORLD_SIZE=str(world), RANK=str(r), LOCAL_RANK=str(r), MASTER_ADDR='127.0.0.1',
+                   MASTER_PORT=port, OMP_NUM_THREADS='1')
+        procs.append(subprocess.Popen([sys.executable, os.path.join(root, 'bench.py')] + args, env=env,
+                                      stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    return procs
+
+
+@pytest.mark.parametrize('mode', ['exit', 'hang'])
+def test_dead_peer_fails_loudly(mode):
+    """rank 1 dies (exit) or stops issuing collectives (hang) at batch 3 of the
+    detection all-gathers; rank 0 must exit non-zero within the process-group timeout, naming its rank
+    and the batch, instead of waiting for an outer kill.  A hung rank is ended by its own watchdog."""
+    import time
+    timeout = 8
+    procs = _start_ranks(2, {'YV7_DIST_FAULT': f'1:3:{mode}', 'YV7_DIST_TIMEOUT_S': str(timeout)},
+                         ['--gpus', '2', '--plumbing', '--model', 'yolov7-tiny', '--batch', '2'])
+    t0 = time.monotonic()
+    outs = []
+    try:
+        for p in procs:
+            outs.append(p.communicate(timeout=240))
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    took = time.monotonic() - t0
+    rc0, rc1 = procs[0].returncode, procs[1].returncode
+    err0 = outs[0][1]
+    assert rc0 != 0 and rc1 != 0, (rc0, rc1, err0[-2000:])
+    assert 'rank 0' in err0 and 'batch 3' in err0, err0[-2000:]
+    if mode == 'exit':
+        assert rc1 == 9
+    else:
+        assert 'rank 1 stalled' in outs[1][1], outs[1][1][-2000:]
+    assert took < 200, took
+
+
+def test_watchdog_fires_on_stall():
+    """yv7.dist.Watchdog in a child process: beats keep it quiet, a stall ends the process with exit code
+    3 and the phase / batch in its message."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ('import sys, time; sys.path[:0] = [%r, %r]\n'
+            'from yv7.dist import Watchdog\n'
+            'w = Watchdog(5, timeout=1.0, poll=0.1)\n'
+            'for i in range(10):\n    w.beat("loop", i); time.sleep(0.3)\n'
+            'w.beat("stuck phase", 42); time.sleep(30)\n') % (os.path.join(root, 'yolo-series_amd'), root)
+    out = subprocess.run([sys.executable, '-c', code], capture_output=True, text=True, timeout=120)
+    assert out.returncode == 3, out.stderr[-2000:]
+    assert 'rank 5 stalled' in out.stderr and 'stuck phase (batch 42)' in out.stderr
+
+
 def test_bench_plumbing_8rank_global_batch_256():
     """BASELINE configs[2] on CPU: `bench.py --gpus 8 --plumbing` — 8 gloo ranks of
     yolov7, 32 images each (global batch 256): every rank receives rank 0's weight blob, the shards are the

@@ -11,8 +11,20 @@ north star names:
   * gather_detections: the fixed-shape per-rank NMS outputs (det [b,300,6] fp32, src_row [b,300]
     int64, count [b] int32) are all-gathered once per batch (~0.3 MB per rank for b = 32) so every
     rank holds the detections of the whole global batch in global image order.
+
+Failure behaviour: a rank that dies or stops issuing collectives must not leave the
+others waiting until an outer kill.  `init` gives the process group a timeout (YV7_DIST_TIMEOUT_S,
+default 120 s) and `Watchdog` ends a rank that makes no host-side progress for that long with exit code
+3 and a line naming the rank, the phase and the batch index; a collective that raises (a peer's
+connection closed) is re-raised with the same attribution by `guarded`.
 """
 from __future__ import annotations
+
+import os
+import sys
+import threading
+import time
+from datetime import timedelta
 
 import torch
 import torch.distributed as dist
@@ -20,6 +32,86 @@ import torch.distributed as dist
 from yv7.graph import compile_model
 from yv7.runtime import Plan
 from yv7 import _lib as L
+
+WATCHDOG_EXIT = 3
+
+
+def timeout_s() -> float:
+    """Seconds a rank may wait on a collective / make no progress (YV7_DIST_TIMEOUT_S, default 120)."""
+    return float(os.environ.get('YV7_DIST_TIMEOUT_S', '120'))
+
+
+def init(backend: str, device=None):
+    """init_process_group with the timeout above (the reference's only collective, train.py:611, is
+    training-only; this is the inference path's)."""
+    kw = {'timeout': timedelta(seconds=timeout_s())}
+    if device is not None:
+        kw['device_id'] = device
+    dist.init_process_group(backend, **kw)
+
+
+class Watchdog:
+    """Host-side progress watchdog for one rank.  `beat(phase, batch)` marks progress (batch = the one
+    about to be issued); if none comes for `timeout` seconds (default 1.25 x timeout_s() + 5) the rank prints `yv7.dist: rank R stalled ... in PHASE (batch K)` to stderr and
+    leaves with os._exit(WATCHDOG_EXIT) — the stuck collective (RCCL all-gather issued on a batch's
+    stream, or a gloo call) can never return, so an orderly exit is not possible.  The host loop blocks
+    on the batches in flight (Inflight reuses a slot only after its previous batch finished), so a
+    stalled all-gather stops the beats within a few batches."""
+
+    def __init__(self, rank: int, timeout: float | None = None, poll: float = 0.5):
+        self.rank = rank
+        # default: past the process group's own timeout, so a collective that raises gets to report first
+        self.timeout = timeout_s() * 1.25 + 5 if timeout is None else timeout
+        self.poll = poll
+        self.phase, self.batch = 'start', None
+        self.last = time.monotonic()
+        self._stop = threading.Event()
+        self._t = threading.Thread(target=self._run, name=f'yv7-watchdog-{rank}', daemon=True)
+        self._t.start()
+
+    def beat(self, phase: str | None = None, batch: int | None = None):
+        if phase is not None:
+            self.phase = phase
+        self.batch = batch
+        self.last = time.monotonic()
+
+    def stop(self):
+        self._stop.set()
+
+    def _run(self):
+        while not self._stop.wait(self.poll):
+            idle = time.monotonic() - self.last
+            if idle > self.timeout:
+                where = self.phase + (f' (batch {self.batch})' if self.batch is not None else '')
+                sys.stderr.write(f'yv7.dist: rank {self.rank} stalled for {idle:.0f} s in {where}: a peer rank '
+                                 f'died or a collective hung; exiting with code {WATCHDOG_EXIT}\n')
+                sys.stderr.flush()
+                os._exit(WATCHDOG_EXIT)
+
+
+def guarded(fn, what: str, batch=None):
+    """Run collective-issuing `fn()`; an exception (a peer's connection closed, the process group's
+    timeout) is re-raised naming this rank, `what` and the batch index."""
+    try:
+        return fn()
+    except Exception as e:  # noqa: BLE001 — re-raised with the rank / batch attribution
+        rk = dist.get_rank() if dist.is_initialized() else -1
+        at = f' of batch {batch}' if batch is not None else ''
+        raise RuntimeError(f'yv7.dist: rank {rk}: {what}{at} failed: {type(e).__name__}: {e}') from e
+
+
+def fault_point(rank: int, batch: int):
+    """Test hook for the failure path (tests/test_dist.py): YV7_DIST_FAULT=R:K:MODE makes rank R, at
+    batch K, exit at once (MODE exit) or stop issuing collectives (MODE hang).  Unset: no effect."""
+    spec = os.environ.get('YV7_DIST_FAULT')
+    if not spec:
+        return
+    r, k, mode = spec.split(':')
+    if int(r) == rank and int(k) == batch:
+        if mode == 'exit':
+            os._exit(9)
+        while True:   # hang: the peers' watchdogs / timeouts must end the job
+            time.sleep(3600)
 
 
 def shard(global_batch: int, rank: int, world: int):
