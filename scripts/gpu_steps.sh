@@ -5,15 +5,18 @@
 # usage: bash scripts/gpu_steps.sh TAG STEP [STEP ...]
 #   tests[=PYTEST_PATHS]        GPU suite (default: tests), -x, per-test timeout       -> tests.log
 #   smoke                       __graft_entry__.smoke()                                -> smoke.log
-#   ops[=NAME][@ENV=V,ENV=V]    serial per-op profile (scripts/op_profile.py) under the env
-#                                                                                     -> ops_NAME.txt
+#   ops[=NAME][@ENV=V,ENV=V]    serial per-op profile (scripts/op_profile.py) under the env; OPS_ARGS adds
+#                               arguments (e.g. OPS_ARGS="--b 64")                    -> ops_NAME.txt
 #   tune=OPS:CANDS[:ROUNDS]     tune_ops.py: each candidate forced on one op at a time -> tune.txt
 #                               (OPS = all for every conv op)
 #   bench[=N][@ENV=V,...]       N bench lines (default 2), --steps 40 --warmup 5  -> bench_STEP_I.json
 #   benchw6[=N][@ENV=V,...]     the same for yolov7-w6 1280 bs 8                  -> benchw6_STEP_I.json
 #   dispatch[=NAME]             scripts/dump_dispatch.py (default dispatch of the 3 bench plans) -> dispatch_NAME.txt
+#   bench/benchw6 take BENCH_ARGS (extra bench.py arguments) from the environment
 #   lib=NAME                    run the following steps on yolo-series_amd/yv7/libyv7_NAME.so (an
 #                               A/B baseline built elsewhere); lib=cur restores the tree's library
+# (round 5's one-shot launchers scripts/gpu_r5*.sh were folded into this driver, gpu_final.sh and
+# gpu_prof.sh; they remain in the git history with the profiles they produced)
 # e.g. bash scripts/gpu_steps.sh r4a tests ops=base ops=nodual@YV7_DUAL=0 tune=8,12:239,234:3 bench=2
 #      bash scripts/gpu_steps.sh r4b ops=new lib=base ops=old lib=cur bench=1 lib=base bench=1 lib=cur
 set -o pipefail
@@ -48,7 +51,7 @@ for step in "$@"; do
       tail -1 $O/smoke.log ;;
     ops)
       f=$O/ops_${arg:-base}.txt
-      env $(envof "$envs") timeout -k 10 300 python -u scripts/op_profile.py --top 100 > $f 2>&1 || { tail $f; exit 1; }
+      env $(envof "$envs") timeout -k 10 300 python -u scripts/op_profile.py --top 100 $OPS_ARGS > $f 2>&1 || { tail $f; exit 1; }
       grep -E "^forward" $f ;;
     tune)
       IFS=: read -r ops cands rounds <<< "$arg"
@@ -59,7 +62,7 @@ for step in "$@"; do
     bench)
       for r in $(seq 1 ${arg:-2}); do
         f=$O/bench_${n}_$r.json
-        env $(envof "$envs") timeout -k 10 300 python -u bench.py --steps 40 --warmup 5 --no-cpu-baseline \
+        env $(envof "$envs") timeout -k 10 300 python -u bench.py  --steps 40 --warmup 5 --no-cpu-baseline $BENCH_ARGS \
           > $f 2> ${f%.json}.err || exit 1
         python -c "import json;d=json.load(open('$f'));print('bench', '$f', '$envs', d['value'], d['detail']['serial_forward_ms'])"
       done ;;

@@ -185,7 +185,10 @@ def test_gpu_fp8_map_parity(name):
     print(f'\n{name} fp8 ({NF} frames): mAP@0.5 vs fp32 oracle {m32:.4f} (oracle fp8 restatement vs fp32: '
           f'{emu32:.4f}), vs fp8 restatement {memu:.4f}; dets/frame {sum(len(d) for d in pred) / NF:.1f}')
     assert m32 >= emu32 - 0.02
-    assert m32 >= {'yolov7': 0.4, 'yolov7-tiny': 0.45}[name]
+    # absolute floors = the 32-frame values measured on MI355X (round 5: yolov7 0.467, tiny 0.592,
+    # profiles/r5_lines/fp8_map.log) minus 0.05 of noise margin (VERDICT r5 item 6 / ADVICE r5); do not
+    # lower them without a failing run that explains why
+    assert m32 >= {'yolov7': 0.42, 'yolov7-tiny': 0.54}[name]
 
 
 @pytest.mark.gpu

@@ -67,7 +67,9 @@ def test_every_conv_variant(name, B, H, W):
 # A net with the shapes the fragment kernels mask: 3x3 layers with cout % 32 == 16 (cout = 80:
 # the permlane16 pair store of the 32-channel pair 64..95 is half masked), stride-2 layers with cin 64
 # and 128 (conv_s2.hip's two weight layouts), and batches with a partial trailing 4-image group after
-# full ones (B = 5, 6).
+# full ones (B = 5, 6).  ADVICE r5: 1x1 layers with the register-weight kernel's input widths (cin 128 /
+# 256 / 512, conv_w1.hip) and outputs of 80 / 144 channels (cout % 32 == 16: masked pair store), so the
+# forced w1 variants really launch on a half-masked N slice and a partial pixel tile (layers 8, 10, 12).
 RAGGED = {'nc': 3, 'depth_multiple': 1.0, 'width_multiple': 1.0,
           'anchors': [[10, 13, 16, 30, 33, 23], [30, 61, 62, 45, 59, 119], [116, 90, 156, 198, 373, 326]],
           'backbone': [[-1, 1, 'Conv', [32, 3, 1]],    # 0  @1
@@ -78,18 +80,28 @@ RAGGED = {'nc': 3, 'depth_multiple': 1.0, 'width_multiple': 1.0,
                        [-1, 1, 'Conv', [128, 1, 1]],   # 5
                        [-1, 1, 'Conv', [80, 3, 2]],    # 6  @8: s2, cin 128 -> 80
                        [-1, 1, 'Conv', [128, 1, 1]],   # 7
-                       [-1, 1, 'Conv', [80, 3, 1]],    # 8  lr, cin 128 -> 80 (P3)
-                       [-1, 1, 'Conv', [64, 1, 1]],    # 9
-                       [-1, 1, 'Conv', [80, 3, 2]],    # 10 @16: s2, cin 64 (P4)
-                       [-1, 1, 'Conv', [128, 1, 1]],   # 11
-                       [-1, 1, 'Conv', [96, 3, 2]]],   # 12 @32: s2, cin 128 (P5)
-          'head': [[[8, 10, 12], 1, 'Detect', ['nc', 'anchors']]]}
+                       [-1, 1, 'Conv', [80, 1, 1]],    # 8  w1, cin 128 -> 80
+                       [-1, 1, 'Conv', [256, 1, 1]],   # 9
+                       [-1, 1, 'Conv', [144, 1, 1]],   # 10 w1, cin 256 -> 144
+                       [-1, 1, 'Conv', [512, 1, 1]],   # 11
+                       [-1, 1, 'Conv', [80, 1, 1]],    # 12 w1, cin 512 -> 80
+                       [-1, 1, 'Conv', [128, 1, 1]],   # 13
+                       [-1, 1, 'Conv', [80, 3, 1]],    # 14 lr, cin 128 -> 80 (P3)
+                       [-1, 1, 'Conv', [64, 1, 1]],    # 15
+                       [-1, 1, 'Conv', [80, 3, 2]],    # 16 @16: s2, cin 64 (P4)
+                       [-1, 1, 'Conv', [128, 1, 1]],   # 17
+                       [-1, 1, 'Conv', [96, 3, 2]]],   # 18 @32: s2, cin 128 (P5)
+          'head': [[[14, 16, 18], 1, 'Detect', ['nc', 'anchors']]]}
+# register-weight 1x1 configurations (conv_w1.hip W1_CFGS) -> the input width each one takes
+W1_CIN = {290: 128, 291: 256, 292: 512, 293: 256, 294: 128, 295: 512, 302: 256, 303: 256}
 
 
 @pytest.mark.parametrize('B', [5, 6])
 def test_fragment_kernels_ragged(B):
     """The fragment kernels (conv_lr.hip 270-279, conv_s2.hip 280-288, conv_w1.hip 290-295, 302-303) on partial
-    trailing image groups / pixel tiles and half-masked channel pairs, op by op against fp32 torch."""
+    trailing image groups / pixel tiles and half-masked channel pairs, op by op against fp32 torch.  A forced
+    w1 variant must actually launch conv1x1_rw_kernel on every 1x1 layer of its input width (no silent
+    fallback to the tuned kernel)."""
     import copy
     from models.yolo import Model
     from yv7.synthetic import synthetic_state_dict
@@ -105,6 +117,13 @@ def test_fragment_kernels_ragged(B):
               290, 291, 292, 293, 294, 295, 302, 303]:
         for i in convs:
             plan.set_op_variant(i, v)
+        if v in W1_CIN:
+            ks = plan.op_kernels(B, H, W)
+            want = [i for i in convs if plan.graph.ops[i].get('k', 1) == 1 and plan.graph.ops[i]['cin'] == W1_CIN[v]
+                    and plan.graph.ops[i]['cout'] % 32 == 16]
+            assert want, f'variant {v}: no 1x1 layer with cin {W1_CIN[v]} and a half-masked channel pair'
+            for i in want:
+                assert any('conv1x1_rw_kernel' in k for k in ks[i]), (v, i, ks[i])
         z, xs = plan.forward(x)
         torch.cuda.synchronize()
         out = check_ops(plan, x, B, H, W, raw=xs, z=z)
@@ -122,8 +141,17 @@ def test_variant_api_rejects_hooks():
     plan = m.plan()
     conv = next(i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV)
     for v in (12, 13, 14, 16, 18, 19, 90, 91, 93, 94, 298, 160, 105, 211, 221, 233, 237, 238, 240, 241,
-              248, 255, 259, 260, 261, 263, 289, 296, 304, 911):
+              248, 255, 259, 260, 261, 263, 289, 296, 299, 300, 301, 304, 911):
         with pytest.raises(RuntimeError):
             plan.set_op_variant(conv, v)
+    # the Detect op: the detbench hooks (91, 93, 95, 96, 98 reach launch_det_pring) are refused, the
+    # alternative heads the suite checks (92, 94, 97, 99) are accepted
+    det = next(i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_DETECT)
+    for v in (91, 93, 95, 96, 98):
+        with pytest.raises(RuntimeError):
+            plan.set_op_variant(det, v)
+    for v in DET_VARIANTS:
+        plan.set_op_variant(det, v)
+    plan.set_op_variant(det, 0)
     with pytest.raises(RuntimeError):
         plan.set_op_variant(len(plan.graph.ops) + 3, 0)

@@ -310,13 +310,15 @@ __global__ __launch_bounds__(512, 2) void conv3x3s2_rw_kernel(const ConvParams p
       // younger than the pieces the next interval needs (issued L - 1 intervals ago): the L - 1 later
       // piece batches and the epilogue stores of intervals q - L + 1 .. q (a tile end among them: this
       // one, or for L = 2 the previous one — the previous tile's last chunk when dc == 0)
+      // (hooks 3 / 4 issue no epilogue stores: NSTW = 0 there)
+      constexpr int NSTW = (HOOK == 3 || HOOK == 4) ? 0 : G::NST;
       if constexpr (HOOK == 1 || HOOK == 2) {
       } else if constexpr (G::L == 1) {
-        if (dc == G::NDC - 1) vmwait<G::NST>();
+        if (dc == G::NDC - 1) vmwait<NSTW>();
         else vmwait<0>();
       } else {
-        if (dc == G::NDC - 1) vmwait<G::PW + G::NST>();
-        else if (dc == 0 && it > 0) vmwait<G::PW + G::NST>();
+        if (dc == G::NDC - 1) vmwait<G::PW + NSTW>();
+        else if (dc == 0 && it > 0) vmwait<G::PW + NSTW>();
         else vmwait<G::PW>();
       }
       barrier();

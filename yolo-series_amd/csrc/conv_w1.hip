@@ -228,8 +228,11 @@ __global__ __launch_bounds__(512, 2) void conv1x1_rw_kernel(const ConvParams p, 
   // vmcnt before the barrier that ends interval v: the pieces of the interval the next barrier opens
   // (issued L - 1 intervals ago) landed; younger: the L - 1 later piece batches and the epilogue stores of
   // intervals v - L + 1 .. v that ended a tile (intervals before the first do not exist)
+  // (hooks: 3 / 4 issue no epilogue stores and 2 no DMA pieces, so those terms are 0 there — ADVICE r5: a
+  // looser count would let a wave past the barrier before its pieces landed and time a racy ring)
   auto wait_next = [&](int v) __attribute__((always_inline)) {
-    constexpr int LB = G::PW * (G::L - 1);
+    constexpr int LB = HOOK == 2 ? 0 : G::PW * (G::L - 1);
+    constexpr int NSTW = (HOOK == 3 || HOOK == 4) ? 0 : G::NST;
     int ends = 0;
 #pragma unroll
     for (int d = 0; d < G::L; ++d) {
@@ -237,9 +240,9 @@ __global__ __launch_bounds__(512, 2) void conv1x1_rw_kernel(const ConvParams p, 
       if (vv >= 0 && vv % G::NIV == G::NIV - 1) ++ends;
     }
     if (ends == 0) vmwait<LB>();
-    else if (ends == 1) vmwait<(LB + G::NST < 63 ? LB + G::NST : 63)>();
-    else if (ends == 2) vmwait<(LB + 2 * G::NST < 63 ? LB + 2 * G::NST : 63)>();
-    else vmwait<(LB + 3 * G::NST < 63 ? LB + 3 * G::NST : 63)>();
+    else if (ends == 1) vmwait<(LB + NSTW < 63 ? LB + NSTW : 63)>();
+    else if (ends == 2) vmwait<(LB + 2 * NSTW < 63 ? LB + 2 * NSTW : 63)>();
+    else vmwait<(LB + 3 * NSTW < 63 ? LB + 3 * NSTW : 63)>();
   };
 
   // ---- prologue

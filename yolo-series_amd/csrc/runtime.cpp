@@ -116,11 +116,13 @@ bool is_f8(const yv7_op_desc& o) { return o.kind == YV7_OP_CONV && o.wfmt == YV7
 // 3x3 / stride-1 or 2 / pad-1 fp16 convs of a shape the fragment kernels accept (conv_lr.hip lr_supported:
 // cin / 32 in {2, 4, 6, 8, 12, 16, 24}, cout % 16 == 0, cout <= 1024; conv_s2.hip: cin 64 / 128) get a
 // fragment-packed weight copy, and so do 1x1 stride-1 convs with 128 / 256 / 512 inputs (conv_w1.hip) —
-// none at all with YV7_LR=0 (the fragment kernels then never run: the forced variants 270-284 / 290-295
-// fall back to the tuned kernel).  Per fp16 plan: yolov7 54.0 MB (3x3 49.8 + 1x1 4.1) beside its 73.9 MB
+// none at all with YV7_FRAG=0 (every fragment kernel then stays off: conv_lr, the register-weight 3x3 / 1x1
+// kernels and the register-weight Detect head; the forced variants 270-288 / 290-295 / 302-303 fall back to
+// the tuned kernel).  YV7_LR=0 only takes conv_lr out of the dispatch (it used to switch the
+// packing, i.e. four kernel families, off at once).  Per fp16 plan: yolov7 54.0 MB (3x3 49.8 + 1x1 4.1) beside its 73.9 MB
 // blob, yolov7-w6 112.4 MB, yolov7-tiny 10.3 MB.
 bool wants_frag(int dtype, const yv7_op_desc& o) {
-  static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
+  static const int lr = [] { const char* e = getenv("YV7_FRAG"); return e ? atoi(e) : 1; }();
   const int nch = o.cin / 32;
   // the Detect head conv with K = 256 / 512 (conv_det_rw_kernel: the weights resident in VGPRs)
   if (dtype == YV7_DT_F16 && o.kind == YV7_OP_DETECT)
