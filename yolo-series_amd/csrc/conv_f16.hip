@@ -2255,6 +2255,32 @@ int conv_splitk_tiles(const ConvParams& p) {
   return (c.cfg < 0 || c.S <= 1) ? 0 : (int)ring_tiles(p, c.cfg);
 }
 
+int lr_default_cfg(const ConvParams& p) {
+  static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
+  if (lr && !p.pool && (long)p.M <= 204800 && p.k == 3 && p.s == 1 &&
+      !((long)p.B * (p.H / 16) * (p.W / 16) >= 800 && ws64_supported(p))) {
+    const bool t5 = p.H % 5 == 0;
+    const long t128 = (long)((p.B + 3) / 4) * (p.H / (t5 ? 5 : 4)) * (p.W / 4) * (p.cout / 128);
+    int cfg = (p.cout % 128 == 0 && t128 >= 400 ? 0 : 1) + (t5 ? 0 : 2);
+    // 160-pixel tiles (10 rows: each weight fragment feeds twice the MFMAs) where they keep >= 400 / 640
+    // blocks (profiles/r4lr/tune_tm10*.txt, us): 160 x 128 for the channel-doubling RepConvs up to 384
+    // inputs (yolov7 128->256 @80 115.5 -> 111.9, 256->512 @40 105.9 -> 100.2; w6 256->512 @80 104.2 ->
+    // 95.9, 384->768 @40 62.2 -> 56.7), 160 x 64 for the other wide / 64-channel layers (512->512 @20
+    // 61.9 -> 57.4, 512->1024 @20 103.8 -> 99.3, 128->64 @80 40.5 -> 37.7, 256->256 @40 56.3 -> 54.9)
+    if (p.H % 10 == 0) {
+      const long g10 = (long)((p.B + 3) / 4) * (p.H / 10) * (p.W / 4);
+      if (p.cout % 128 == 0 && p.cout >= 2 * p.cin && p.cin <= 384 && g10 * (p.cout / 128) >= 400) cfg = 5;
+      else if (p.cout != 128 && p.cout % 64 == 0 && g10 * (p.cout / 64) >= 480) cfg = 6;
+    }
+    // Round 5 (profiles/r5_misc/tune_small_w6.txt, us): 160 x 64 from 480 such tiles (w6 bs 8 384->384 @40
+    // 38.0 / 37.9 / 37.1 / 37.3 -> 35.6-35.9); 64-pixel tiles on the 3 200-pixel layers (w6 bs 8 @20:
+    // 512->512 25.3 / 25.0 / 25.2 -> 23.7-24.1, 512->256 18.4 -> 17.1, 256->256 11.3 -> 10.4)
+    if (cfg == 1 && p.M <= 6400 && lr_supported(p, 3)) cfg = 3;
+    if (lr_supported(p, cfg)) return cfg;
+  }
+  return -1;
+}
+
 hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   const bool one = p.k == 1 && p.s == 1 && p.pad == 0;
   const int variant = p.variant ? p.variant : env_variant();
@@ -2274,6 +2300,8 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     return launch_conv_hring(p, device_cus(), st);
   // the low-resolution 3x3 kernel (conv_lr.hip): 270 + tile configuration
   if (!det && variant >= 270 && variant <= 279 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
+  // its configurations 10-13 (the patch two chunks ahead): 306-309
+  if (!det && variant >= 306 && variant <= 309 && lr_supported(p, variant - 296)) return launch_conv_lr(p, variant - 296, st);
   // the register-weight stride-2 kernel (conv_s2.hip): 280 + tile configuration
   if (!det && variant >= 280 && variant <= 288 && s2_supported(p, variant - 280))
     return launch_conv_s2(p, variant - 280, device_cus(), st);
@@ -2307,26 +2335,9 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
   // 73.0 -> 66.0 with 80 x 128 (480 / 960 tiles); yolov7's 512->512 @20 and 128->128 / 256->128 @40
   // (640) are equal either way.  YV7_LR=0: off.
   static const int lr = [] { const char* e = getenv("YV7_LR"); return e ? atoi(e) : 1; }();
-  if (!det && variant == 0 && lr && (long)p.M <= 204800 && p.k == 3 && p.s == 1 &&
-      !((long)p.B * (p.H / 16) * (p.W / 16) >= 800 && ws64_supported(p))) {
-    const bool t5 = p.H % 5 == 0;
-    const long t128 = (long)((p.B + 3) / 4) * (p.H / (t5 ? 5 : 4)) * (p.W / 4) * (p.cout / 128);
-    int cfg = (p.cout % 128 == 0 && t128 >= 400 ? 0 : 1) + (t5 ? 0 : 2);
-    // 160-pixel tiles (10 rows: each weight fragment feeds twice the MFMAs) where they keep >= 400 / 640
-    // blocks (profiles/r4lr/tune_tm10*.txt, us): 160 x 128 for the channel-doubling RepConvs up to 384
-    // inputs (yolov7 128->256 @80 115.5 -> 111.9, 256->512 @40 105.9 -> 100.2; w6 256->512 @80 104.2 ->
-    // 95.9, 384->768 @40 62.2 -> 56.7), 160 x 64 for the other wide / 64-channel layers (512->512 @20
-    // 61.9 -> 57.4, 512->1024 @20 103.8 -> 99.3, 128->64 @80 40.5 -> 37.7, 256->256 @40 56.3 -> 54.9)
-    if (p.H % 10 == 0) {
-      const long g10 = (long)((p.B + 3) / 4) * (p.H / 10) * (p.W / 4);
-      if (p.cout % 128 == 0 && p.cout >= 2 * p.cin && p.cin <= 384 && g10 * (p.cout / 128) >= 400) cfg = 5;
-      else if (p.cout != 128 && p.cout % 64 == 0 && g10 * (p.cout / 64) >= 480) cfg = 6;
-    }
-    // Round 5 (profiles/r5_misc/tune_small_w6.txt, us): 160 x 64 from 480 such tiles (w6 bs 8 384->384 @40
-    // 38.0 / 37.9 / 37.1 / 37.3 -> 35.6-35.9); 64-pixel tiles on the 3 200-pixel layers (w6 bs 8 @20:
-    // 512->512 25.3 / 25.0 / 25.2 -> 23.7-24.1, 512->256 18.4 -> 17.1, 256->256 11.3 -> 10.4)
-    if (cfg == 1 && p.M <= 6400 && lr_supported(p, 3)) cfg = 3;
-    if (lr_supported(p, cfg)) return launch_conv_lr(p, cfg, st);
+  if (!det && variant == 0) {
+    const int cfg = lr_default_cfg(p);
+    if (cfg >= 0) return launch_conv_lr(p, cfg, st);
   }
   // 3x3 stride-2 layers with 64 / 128 input channels and at least 204 800 output pixels: the register-weight
   // stride-2 kernel (conv_s2.hip).  In-network, one layer forced at a time (scripts/tune_ops.py,

@@ -45,53 +45,68 @@ __host__ __device__ constexpr int swz(int img) { return (0x1320 >> (4 * img)) & 
 template <int S> __host__ __device__ constexpr int patch_cols() { return S == 1 ? FC + 2 : 2 * FC + 1; }
 template <int S> __host__ __device__ constexpr int col_slot(int c) { return S == 1 ? c : ((c & 1) ? 5 + (c >> 1) : (c >> 1)); }
 
-// WM x WN waves; wave (wm, wn) owns output rows wm*TM .. wm*TM+TM-1 of the tile and channels
-// n0 + wn*TN*16 .. +TN*16; PD = weight prefetch distance in column steps (3 per chunk); S = stride
-// (2: tap (r, s) of output (y, x) is input (2y - 1 + r, 2x - 1 + s): a wave reads patch rows
-// 2*wm*TM .. 2*wm*TM + 2*TM once per column step, output row i taking rows 2i + r).  Images past B
-// (B not a multiple of 4) read zeros (past the input's buffer range) and store nothing.
-template <int WM, int WN, int TN, int TM, int NCH, int ACT, int PD, int S>
-__global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) : 1) void conv3x3_lr_kernel(const ConvParams p, int ngx) {
-  constexpr int NT = 64 * WM * WN;
-  constexpr int TH = TM * WM, PR = S * TH + 3 - S, PC = patch_cols<S>();
+// Tile geometry of a configuration (see conv3x3_lr_kernel).
+template <int WM, int WN, int TM, int S>
+struct LrGeo {
+  static constexpr int NT = 64 * WM * WN;
+  static constexpr int TH = TM * WM, PR = S * TH + 3 - S, PC = patch_cols<S>();
+  static constexpr int PPX = FI * PR * PC;       // patch pixels
+  static constexpr int PB = PPX * 64;            // bytes per patch buffer
+};
+
+// tile configurations {WM, WN, TN, TM, PD, S} (variants 270 + row): pixels 16 * WM * TM x channels
+// 16 * WN * TN, weights PD column steps ahead, stride S.  Kept from the round-4 sweep of 20 stride-1
+// configurations (profiles/r4lr/tune{1,2,3}.txt, one layer forced at a time in the yolov7 bs-32
+// forward): 4-wave blocks of 80-pixel tiles with the weights three column steps ahead won every layer
+// shape; the 8-wave and 128 / 160-pixel tiles, and two steps of prefetch, lost by 5-20 %.  0: 80 x 128,
+// 1: 80 x 64; 2 / 3: the same with 64-pixel tiles for heights that 5 does not divide.  4: stride 2,
+// 64 x 128.  At stride 2 the same four were correct but slower than the dispatch on the large yolov7
+// stride-2 layers (profiles/r4lr/convbench_s2.txt: 64->128 s2 @320 243 vs 215 us, 256->256 s2 @80 77
+// vs 68: a 9-column, 2*TH+1-row patch per output tile is 4-5 input pixels per output against 2.1 at
+// stride 1) and faster only where the dispatch split K: 256->256 s2 @40 25.4 vs 29.6.  5 / 6: 160-pixel
+// tiles (TH = 10) of 128 / 64 channels (profiles/r4lr/tune_tm10*.txt: 3-9 % on the wide layers).
+// Round 5, stride 2 (profiles/r5_s2/cb_deep_s2.txt, tune_deep_*.txt): 7 = 80 x 128 (5 rows) wins on the
+// w6 12 800-pixel layers with cout >= 384 (512->768 s2 @80 109.1 -> 101.5 us in-network); 8 = 128 x 128
+// (8 rows, PD 2) and 9 = 160 x 64 lost everywhere (VGPR-bound weight prefetch, LDS-read bound) and are
+// kept only as forced variants.
+// Reading the next column step's patch rows before this step's MFMAs (two register sets; across a
+// chunk boundary after the barrier) was no faster on any layer and cost a wave per SIMD
+// (profiles/r4lr/tune_xp.txt): three waves per SIMD already hide the LDS latency.
+// Round 6 (PF = 2, rows 10-13, variants 306-309): rows 0 / 1 / 3 / 6 with the input patch loaded two
+// chunks ahead (two register sets) instead of one — at 20^2 / 40^2 a layer's ~640 tiles leave 2-3 waves per
+// SIMD, too few to hide a chunk's HBM / MALL latency behind one chunk of MFMAs (profiles/r6_diag_batch/:
+// these layers run 17-37 % faster per image at bs 64 / 128).
+#define LR_CFGS(X)                                                                                   \
+  X(0, 1, 4, 2, 5, 3, 1, 1) X(1, 1, 4, 1, 5, 3, 1, 1) X(2, 1, 4, 2, 4, 3, 1, 1) X(3, 1, 4, 1, 4, 3, 1, 1)          \
+  X(4, 1, 4, 2, 4, 3, 2, 1) X(5, 1, 4, 2, 10, 2, 1, 1) X(6, 1, 4, 1, 10, 3, 1, 1) X(7, 1, 4, 2, 5, 3, 2, 1)        \
+  X(8, 1, 4, 2, 8, 2, 2, 1) X(9, 1, 4, 1, 10, 3, 2, 1) X(10, 1, 4, 2, 5, 3, 1, 2) X(11, 1, 4, 1, 5, 3, 1, 2)      \
+  X(12, 1, 4, 1, 4, 3, 1, 2) X(13, 1, 4, 1, 10, 3, 1, 2)
+#define LR_ROW(i, wm, wn, tn, tm, pd, s, pf) {wm, wn, tn, tm, pd, s, pf},
+constexpr int LR_CFG[][7] = {LR_CFGS(LR_ROW)};
+constexpr int LR_NCFG = sizeof(LR_CFG) / sizeof(LR_CFG[0]);
+
+// One output tile: images b0 .. b0 + 3, rows y0 .. y0 + TH - 1, columns x0 .. x0 + 3, channels n0 .. n0 + BN - 1
+// (the body of conv3x3_lr_kernel, shared with the chain kernel of conv_chain.hip).  CPL / CPS: cache policy of
+// the patch loads / output stores (0, or CPOL_SC1 for an in-launch hand-off between chained layers); `ready`
+// runs before the first load of the tile (the chain kernel waits there for the producing layer's rows).
+template <int WM, int WN, int TN, int TM, int NCH, int ACT, int PD, int S, int PF = 1, int CPL = 0, int CPS = 0,
+          typename R>
+__device__ __forceinline__ void lr_tile(const ConvParams& p, int b0, int y0, int x0, int n0, unsigned char* smem,
+                                        R&& ready) {
+  using G = LrGeo<WM, WN, TM, S>;
+  constexpr int NT = G::NT;
+  constexpr int PR = G::PR, PC = G::PC;
   constexpr int NXA = S * TM + 3 - S;            // patch rows a wave reads per column step
-  constexpr int PPX = FI * PR * PC;              // patch pixels
-  constexpr int PB = PPX * 64;                   // bytes per patch buffer
-  constexpr int BN = WN * TN * 16;
+  constexpr int PPX = G::PPX;
+  constexpr int PB = G::PB;
   constexpr int NPL = (PPX * 4 + NT - 1) / NT;   // 16-byte patch pieces per thread per chunk
   constexpr int NPH = 3 * NCH;                   // column steps ("phases")
   constexpr int NWB = PD + 1;                    // weight register buffers
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PB];
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int g = lane >> 4, li = lane & 15;
-
-  // tile: XCD-aware (blockIdx % 8 is the XCD on the round-robin dispatch).  The 8 XCDs form ngx N groups
-  // x 8 / ngx pixel groups: XCD x holds N slices (x % ngx) * nN / ngx .. + nN / ngx (its share of the
-  // weights stays in its 4 MiB L2: ngx is chosen so that share is <= 2.5 MiB) and the (x / ngx)-th
-  // contiguous range of pixel tiles (neighbours share patch halos).  ngx = 1: every XCD streams all
-  // slices over its eighth of the pixels (VERDICT r4 item 3: the 4.7-9.4 MB weights of the 512-input
-  // layers re-fetched from MALL/HBM per tile on every XCD, 5.3x the algorithmic bytes).
-  const int bid = blockIdx.x;
-  const int nN = (p.cout + BN - 1) / BN;
-  const int ncg = p.Wo / FC;
-  const int nrg_ = p.Ho / TH, nig = (p.B + FI - 1) / FI;
-  const int P = nig * nrg_ * ncg;               // pixel tiles
-  const int npx = 8 / ngx, nsl = nN / ngx;      // pixel groups, N slices per XCD
-  const int xcd = bid % 8, k = bid / 8;
-  const int pper = (P + npx - 1) / npx;         // pixel tiles per pixel group
-  const int pi = (xcd / ngx) * pper + k / nsl;
-  if (k / nsl >= pper || pi >= P) return;       // (the grid is 8 * nsl * pper blocks)
-  const int nt = (xcd % ngx) * nsl + k % nsl;
-  int t = pi;
-  const int x0 = (t % ncg) * FC;
-  t /= ncg;
-  const int nrg = p.Ho / TH;   // (t / nrg: image group, ceil(B / 4) of them)
-  const int y0 = (t % nrg) * TH;
-  const int b0 = (t / nrg) * FI;
-  const int n0 = nt * BN;
 
   const auto xr = make_rsrc(p.x, p.xbytes);
   const auto wr = make_rsrc(p.wf, p.wfbytes);
@@ -113,16 +128,17 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
       pd[k] = 0xffffffffu;
     }
   }
-  u4 pr[NPL];
+  // chunk c's patch pieces travel in register set c % PF (PF = 2: loaded two chunks ahead of its LDS store)
+  u4 pr[PF][NPL];
   auto load_patch = [&](int c) __attribute__((always_inline)) {
 #pragma unroll
     for (int k = 0; k < NPL; ++k)
-      pr[k] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, po[k], (uint32_t)(c * CK * 2), 0));
+      pr[c % PF][k] = __builtin_bit_cast(u4, __builtin_amdgcn_raw_buffer_load_b128(xr, po[k], (uint32_t)(c * CK * 2), CPL));
   };
-  auto store_patch = [&](int buf) __attribute__((always_inline)) {
+  auto store_patch = [&](int c) __attribute__((always_inline)) {   // chunk c into LDS buffer c & 1
 #pragma unroll
     for (int k = 0; k < NPL; ++k)
-      if (pd[k] != 0xffffffffu) *reinterpret_cast<u4*>(smem + buf * PB + pd[k]) = pr[k];
+      if (pd[k] != 0xffffffffu) *reinterpret_cast<u4*>(smem + (c & 1) * PB + pd[k]) = pr[c % PF][k];
   };
 
   // ---- weight fragments: (nf, chunk, tap) at ((nf * NCH + c) * 9 + tap) KiB, lane-linear
@@ -158,13 +174,16 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
   const uint32_t a_lane = (uint32_t)(((img * PR) * PC + (li & 3)) * 64 + ((g ^ swz(img)) * 16));
   const uint32_t a_wave = (uint32_t)(S * wm * TM * PC * 64);
 
-  // ---- prologue: chunk 0's patch into buffer 0, chunk 1's in registers, PD phases of weights
+  // ---- prologue: chunk 0's patch into buffer 0, chunks 1 .. PF in registers, PD phases of weights
+  ready();
   load_patch(0);
 #pragma unroll
   for (int ph = 0; ph < PD; ++ph)
     if (ph < NPH) load_w(ph, wreg[ph]);
   store_patch(0);
-  if constexpr (NCH > 1) load_patch(1);
+#pragma unroll
+  for (int c = 1; c <= PF; ++c)
+    if (c < NCH) load_patch(c);
   __syncthreads();
 
   // patch rows of column step (c, s): the lane's column 2x + s (S = 2) or x + s sits in slot
@@ -196,8 +215,8 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
       mfmas(ph, xa);
     }
     if (c + 1 < NCH) {
-      store_patch((c + 1) & 1);   // buffer of chunk c - 1: every wave left it at the last barrier
-      if (c + 2 < NCH) load_patch(c + 2);
+      store_patch(c + 1);   // buffer of chunk c - 1: every wave left it at the last barrier
+      if (c + 1 + PF < NCH) load_patch(c + 1 + PF);   // into the register set chunk c + 1 just left
       __syncthreads();
     }
   }
@@ -226,7 +245,7 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
         const auto s1 = __builtin_amdgcn_permlane16_swap(a[1], b[1], false, false);
         const u4 v = {s0[0], s1[0], s0[1], s1[1]};
         const int n = n0 + wn * TN * 16 + mp * 32 + (int)lane_ch;
-        __builtin_amdgcn_raw_buffer_store_b128(v, yr, (live && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu, 0, 0);
+        __builtin_amdgcn_raw_buffer_store_b128(v, yr, (live && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu, 0, CPS);
       }
     } else {
 #pragma unroll
@@ -236,11 +255,219 @@ __global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) :
         for (int e = 0; e < 4; ++e) va[e] = (_Float16)act_t<ACT>(acc[j][i][e]);
         const int n = n0 + wn * TN * 16 + j * 16 + g * 4;
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u2, va), yr,
-                                              (live && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu, 0, 0);
+                                              (live && n < p.cout) ? yo + (uint32_t)n * 2 : 0xffffffffu, 0, CPS);
       }
     }
   }
 }
+
+// WM x WN waves; wave (wm, wn) owns output rows wm*TM .. wm*TM+TM-1 of the tile and channels
+// n0 + wn*TN*16 .. +TN*16; PD = weight prefetch distance in column steps (3 per chunk); S = stride
+// (2: tap (r, s) of output (y, x) is input (2y - 1 + r, 2x - 1 + s): a wave reads patch rows
+// 2*wm*TM .. 2*wm*TM + 2*TM once per column step, output row i taking rows 2i + r).  Images past B
+// (B not a multiple of 4) read zeros (past the input's buffer range) and store nothing.
+template <int WM, int WN, int TN, int TM, int NCH, int ACT, int PD, int S, int PF>
+__global__ __launch_bounds__(64 * WM * WN, (8 / (WM * WN)) > 0 ? 8 / (WM * WN) : 1) void conv3x3_lr_kernel(const ConvParams p, int ngx) {
+  using G = LrGeo<WM, WN, TM, S>;
+  constexpr int TH = G::TH;
+  constexpr int BN = WN * TN * 16;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * G::PB];
+
+  // tile: XCD-aware (blockIdx % 8 is the XCD on the round-robin dispatch).  The 8 XCDs form ngx N groups
+  // x 8 / ngx pixel groups: XCD x holds N slices (x % ngx) * nN / ngx .. + nN / ngx (its share of the
+  // weights stays in its 4 MiB L2: ngx is chosen so that share is <= 2.5 MiB) and the (x / ngx)-th
+  // contiguous range of pixel tiles (neighbours share patch halos).  ngx = 1: every XCD streams all
+  // slices over its eighth of the pixels (VERDICT r4 item 3: the 4.7-9.4 MB weights of the 512-input
+  // layers re-fetched from MALL/HBM per tile on every XCD, 5.3x the algorithmic bytes).
+  const int bid = blockIdx.x;
+  const int nN = (p.cout + BN - 1) / BN;
+  const int ncg = p.Wo / FC;
+  const int nrg_ = p.Ho / TH, nig = (p.B + FI - 1) / FI;
+  const int P = nig * nrg_ * ncg;               // pixel tiles
+  const int npx = 8 / ngx, nsl = nN / ngx;      // pixel groups, N slices per XCD
+  const int xcd = bid % 8, k = bid / 8;
+  const int pper = (P + npx - 1) / npx;         // pixel tiles per pixel group
+  const int pi = (xcd / ngx) * pper + k / nsl;
+  if (k / nsl >= pper || pi >= P) return;       // (the grid is 8 * nsl * pper blocks)
+  const int nt = (xcd % ngx) * nsl + k % nsl;
+  int t = pi;
+  const int x0 = (t % ncg) * FC;
+  t /= ncg;
+  const int nrg = p.Ho / TH;   // (t / nrg: image group, ceil(B / 4) of them)
+  const int y0 = (t % nrg) * TH;
+  const int b0 = (t / nrg) * FI;
+  lr_tile<WM, WN, TN, TM, NCH, ACT, PD, S, PF>(p, b0, y0, x0, nt * BN, smem, [] {});
+}
+
+// ---------------------------------------------------------------------------------------------
+// Chained low-resolution 3x3 layers.  At 20^2 / 40^2 (bs 32) one such layer is 12 800 /
+// 51 200 output pixels: its 640 tiles are about one round of the chip's block slots, so every layer pays its
+// own ramp, its tail (the CUs idle behind the last tiles) and a kernel boundary; the same layers run 22-37 %
+// faster per image at bs 64 / 128 (profiles/r6_diag_batch/).  One launch runs the whole 3x3 stack of an ELAN
+// block: a dynamic queue hands out tasks (layer, image group, row band, column group, N slice) in layer
+// order; a task of layer l + 1 waits only for the row bands of layer l its 3x3 window reads (rows y0 - 1 ..
+// y0 + TH of its four images, every column group and N slice), so the next layer's tiles fill the CUs the
+// current layer's tail leaves idle.  Deadlock-free for any residency: a task only waits for tasks with
+// smaller queue indices, all handed to blocks that were running when they took them.
+//
+// Hand-off (MI355X_MICROARCH.md, inter-workgroup visibility, the sc1 form, row 1): a producing layer stores
+// its tile with 16-byte sc1 (write-through) stores, every wave waits vmcnt(0), a workgroup barrier, then one
+// lane adds 1 to the band's counter (agent-scope atomic); the consumer's lane 0 polls the counters with sc1
+// loads (s_sleep between polls), a workgroup barrier, and every load of the handed-off rows is a 16-byte sc1
+// buffer load to registers.  The last block to finish re-arms the queue and counters for the next launch.
+// Counters (ints, one 128-byte line each): [0] queue head, [32] blocks done, [64] timeout flag (sticky),
+// [96 + 32 k] band k: layer l's bands (image group ig, band b) at k = off_l + ig * nrg_l + b, l < nl - 1.
+constexpr int CPOL_SC1 = 16;
+constexpr int CH_HEAD = 0, CH_DONE = 32, CH_ERR = 64, CH_BAND0 = 96, CH_LINE = 32;
+
+template <int C>
+struct LrCfg {
+  static constexpr int WM = LR_CFG[C][0], WN = LR_CFG[C][1], TN = LR_CFG[C][2], TM = LR_CFG[C][3],
+                       PD = LR_CFG[C][4], S = LR_CFG[C][5], PF = LR_CFG[C][6];
+  static constexpr int TH = WM * TM, BN = WN * TN * 16, NT = 64 * WM * WN;
+  static constexpr int PB = LrGeo<WM, WN, TM, S>::PB;
+};
+
+// per-layer geometry of a chain (host and device)
+struct ChainGeo {
+  int nl, nig, ncg;
+  int th[CHAIN_MAX], bn[CHAIN_MAX], nrg[CHAIN_MAX], nN[CHAIN_MAX], t0[CHAIN_MAX + 1], boff[CHAIN_MAX + 1];
+};
+__host__ __device__ inline ChainGeo chain_geo(const ChainParams& c) {
+  ChainGeo g;
+  g.nl = c.nl;
+  g.nig = (c.p[0].B + FI - 1) / FI;
+  g.ncg = c.p[0].Wo / FC;
+  g.t0[0] = 0;
+  g.boff[0] = 0;
+  for (int l = 0; l < CHAIN_MAX; ++l) {
+    const int cfg = l == 0 ? c.cfg0 : c.cfg1;
+    const bool on = l < c.nl;
+    g.th[l] = LR_CFG[cfg][0] * LR_CFG[cfg][3];
+    g.bn[l] = LR_CFG[cfg][1] * LR_CFG[cfg][2] * 16;
+    g.nrg[l] = on ? c.p[l].Ho / g.th[l] : 0;
+    g.nN[l] = on ? (c.p[l].cout + g.bn[l] - 1) / g.bn[l] : 0;
+    g.t0[l + 1] = g.t0[l] + g.nig * g.nrg[l] * g.ncg * g.nN[l];
+    g.boff[l + 1] = g.boff[l] + (l + 1 < c.nl ? g.nig * g.nrg[l] : 0);
+  }
+  return g;
+}
+
+template <int C0, int N0, int C1, int N1, int ACT>
+__global__ __launch_bounds__(256, 3) void conv3x3_chain_kernel(const ChainParams cp) {
+  using A = LrCfg<C0>;
+  using Bc = LrCfg<C1>;
+  static_assert(A::NT == 256 && Bc::NT == 256 && A::S == 1 && Bc::S == 1, "4-wave stride-1 configurations");
+  constexpr int PBM = A::PB > Bc::PB ? A::PB : Bc::PB;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * PBM];
+  __shared__ int task_s[2], last_s;
+  // per layer in LDS (dynamic indexing of a register array would put it in scratch): tiles before it (t0),
+  // row bands, N slices, its first band counter (boff)
+  __shared__ int t0[CHAIN_MAX + 1], nrg_[CHAIN_MAX], nN_[CHAIN_MAX], boff_[CHAIN_MAX];
+  int* const ctr = cp.ctr;
+  const int tid = threadIdx.x;
+  const int nl = cp.nl;
+  const int nig = (cp.p[0].B + FI - 1) / FI, ncg = cp.p[0].Wo / FC, Ho = cp.p[0].Ho;
+  if (tid == 0) {
+    int ta = 0, bo = 0;
+    t0[0] = 0;
+#pragma unroll
+    for (int l = 0; l < CHAIN_MAX; ++l) {
+      const bool on = l < nl;
+      const int th = l == 0 ? A::TH : Bc::TH, bn = l == 0 ? A::BN : Bc::BN;
+      const int nrg = on ? Ho / th : 0, nN = on ? (cp.p[l].cout + bn - 1) / bn : 0;
+      nrg_[l] = nrg;
+      nN_[l] = nN;
+      boff_[l] = bo;
+      bo += nig * nrg;
+      ta += nig * nrg * ncg * nN;
+      t0[l + 1] = ta;
+    }
+  }
+  __syncthreads();
+  const int total = t0[nl];
+
+  for (int it = 0;; ++it) {
+    if (tid == 0) task_s[it & 1] = __hip_atomic_fetch_add(ctr + CH_HEAD, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();   // also: every wave is done with the previous task's LDS
+    const int t = task_s[it & 1];
+    if (t >= total) break;
+    int l = 0;
+    while (l + 1 < nl && t >= t0[l + 1]) ++l;
+    l = __builtin_amdgcn_readfirstlane(l);
+    int u = t - t0[l];
+    const int nN = nN_[l], nrg = nrg_[l], th = l == 0 ? A::TH : Bc::TH;
+    const int nt = u % nN;
+    u /= nN;
+    const int cg = u % ncg;
+    u /= ncg;
+    const int band = u % nrg, ig = u / nrg;
+    const int b0 = ig * FI, y0 = band * th, x0 = cg * FC, n0 = nt * (l == 0 ? A::BN : Bc::BN);
+    const ConvParams& p = cp.p[l];
+    // layer l - 1's bands holding rows y0 - 1 .. y0 + th of image group ig, each complete when all of its
+    // column groups and N slices have signalled
+    auto ready = [&]() __attribute__((always_inline)) {
+      if (l > 0) {
+        if (tid == 0) {
+          const int pth = l == 1 ? A::TH : Bc::TH, pnrg = nrg_[l - 1];
+          const int lo = (y0 > 0 ? y0 - 1 : 0) / pth;
+          const int hi = (y0 + th < Ho ? y0 + th : Ho - 1) / pth;
+          const int target = ncg * nN_[l - 1];
+          int* c = ctr + CH_BAND0 + CH_LINE * (boff_[l - 1] + ig * pnrg);
+          for (int b = lo; b <= hi; ++b) {
+            int spins = 0;
+            while (__hip_atomic_load(c + CH_LINE * b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+              __builtin_amdgcn_s_sleep(2);
+              if (++spins > (1 << 24)) {   // ~1 s: a lost signal would otherwise hang the GPU
+                __hip_atomic_store(ctr + CH_ERR, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                break;
+              }
+            }
+          }
+        }
+        __syncthreads();
+      }
+    };
+    if (l == 0)
+      lr_tile<A::WM, A::WN, A::TN, A::TM, N0, ACT, A::PD, 1, A::PF, 0, CPOL_SC1>(p, b0, y0, x0, n0, smem, ready);
+    else if (l + 1 < nl)
+      lr_tile<Bc::WM, Bc::WN, Bc::TN, Bc::TM, N1, ACT, Bc::PD, 1, Bc::PF, CPOL_SC1, CPOL_SC1>(p, b0, y0, x0, n0, smem, ready);
+    else
+      lr_tile<Bc::WM, Bc::WN, Bc::TN, Bc::TM, N1, ACT, Bc::PD, 1, Bc::PF, CPOL_SC1, 0>(p, b0, y0, x0, n0, smem, ready);
+    if (l + 1 < nl) {   // publish: this tile's rows are in memory
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0)
+        __hip_atomic_fetch_add(ctr + CH_BAND0 + CH_LINE * (boff_[l] + ig * nrg + band), 1, __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  // re-arm: the block that finishes last (every other block has made its last counter access) zeroes the
+  // queue head, the done count and the band counters for the next launch
+  if (tid == 0) last_s = __hip_atomic_fetch_add(ctr + CH_DONE, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+                         (int)gridDim.x - 1;
+  __syncthreads();
+  if (last_s) {
+    const int nb = boff_[nl - 1];
+    for (int k = tid; k < nb; k += 256)
+      __hip_atomic_store(ctr + CH_BAND0 + CH_LINE * k, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0) {
+      __hip_atomic_store(ctr + CH_HEAD, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ctr + CH_DONE, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// the (layer-0 configuration, its chunks, later layers' configuration, their chunks) instantiated: the
+// ELAN 3x3 stacks of yolov7 bs 32 at 640 (20^2: 256 -> 256, and 512 -> 256 then 256 -> 256; 40^2: 256 ->
+// 128 then 128 -> 128) and yolov7-w6 bs 8 at 1280 (its 40^2 and 20^2 stacks: 384 / 512 / 192 / 256
+// channels), all on 80 x 64 tiles (configuration 1) or 64 x 64 (3, heights 5 does not divide); the
+// runtime gives a chain 80 x 64 tiles where the single-layer dispatch would take 80 x 128 (equal there
+// per layer, profiles/r4lr/tune3.txt; twice the tasks for the queue, and the 128-channel form's 160
+// VGPRs leave no room for the chain's state at 3 blocks per CU)
+#define CHAIN_FORMS(X)                                                                                \
+  X(1, 8, 1, 8) X(1, 16, 1, 8) X(1, 8, 1, 4) X(1, 12, 1, 12) X(3, 16, 3, 16) X(3, 12, 3, 16) X(1, 24, 1, 12) \
+  X(1, 6, 1, 6) X(1, 12, 1, 6) X(3, 24, 3, 16) X(1, 16, 1, 16) X(1, 4, 1, 4)
 
 // Fragment packing: out[((nf * nch + c) * T + tap) * 512 + lane * 8 + e] =
 // w[(nf * 16 + lane % 16) * kpad + tap * cin + c * 32 + (lane / 16) * 8 + e] — the MFMA A operand of
@@ -260,7 +487,7 @@ __global__ void pack_frag_kernel(const _Float16* w, int kpad, int cin, int nfrag
   }
 }
 
-template <int WM, int WN, int TN, int TM, int PD, int S, int NCH>
+template <int WM, int WN, int TN, int TM, int PD, int S, int PF, int NCH>
 hipError_t launch_cfg(const ConvParams& p, hipStream_t st) {
   constexpr int TH = TM * WM, BN = WN * TN * 16;
   const long P = (long)((p.B + FI - 1) / FI) * (p.Ho / TH) * (p.Wo / FC);
@@ -278,50 +505,26 @@ hipError_t launch_cfg(const ConvParams& p, hipStream_t st) {
   if (ngx < 1 || 8 % ngx || nN % ngx) ngx = 1;
   const int npx = 8 / ngx, nsl = nN / ngx;
   const long grid = 8L * nsl * ((P + npx - 1) / npx);
-  if (p.act == 1) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 1, PD, S>), dim3((unsigned)grid), dim3(64 * WM * WN), 0, st, p, ngx);
-  else if (p.act == 2) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 2, PD, S>), dim3((unsigned)grid), dim3(64 * WM * WN), 0, st, p, ngx);
-  else YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 0, PD, S>), dim3((unsigned)grid), dim3(64 * WM * WN), 0, st, p, ngx);
+  if (p.act == 1) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 1, PD, S, PF>), dim3((unsigned)grid), dim3(64 * WM * WN), 0, st, p, ngx);
+  else if (p.act == 2) YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 2, PD, S, PF>), dim3((unsigned)grid), dim3(64 * WM * WN), 0, st, p, ngx);
+  else YV7_LAUNCH((conv3x3_lr_kernel<WM, WN, TN, TM, NCH, 0, PD, S, PF>), dim3((unsigned)grid), dim3(64 * WM * WN), 0, st, p, ngx);
   return hipGetLastError();
 }
 
-template <int WM, int WN, int TN, int TM, int PD, int S>
+template <int WM, int WN, int TN, int TM, int PD, int S, int PF>
 hipError_t launch_nch(const ConvParams& p, hipStream_t st) {
   switch (p.cin / CK) {
-    case 2: return launch_cfg<WM, WN, TN, TM, PD, S, 2>(p, st);
-    case 4: return launch_cfg<WM, WN, TN, TM, PD, S, 4>(p, st);
-    case 6: return launch_cfg<WM, WN, TN, TM, PD, S, 6>(p, st);
-    case 8: return launch_cfg<WM, WN, TN, TM, PD, S, 8>(p, st);
-    case 12: return launch_cfg<WM, WN, TN, TM, PD, S, 12>(p, st);
-    case 16: return launch_cfg<WM, WN, TN, TM, PD, S, 16>(p, st);
-    case 24: return launch_cfg<WM, WN, TN, TM, PD, S, 24>(p, st);
+    case 2: return launch_cfg<WM, WN, TN, TM, PD, S, PF, 2>(p, st);
+    case 4: return launch_cfg<WM, WN, TN, TM, PD, S, PF, 4>(p, st);
+    case 6: return launch_cfg<WM, WN, TN, TM, PD, S, PF, 6>(p, st);
+    case 8: return launch_cfg<WM, WN, TN, TM, PD, S, PF, 8>(p, st);
+    case 12: return launch_cfg<WM, WN, TN, TM, PD, S, PF, 12>(p, st);
+    case 16: return launch_cfg<WM, WN, TN, TM, PD, S, PF, 16>(p, st);
+    case 24: return launch_cfg<WM, WN, TN, TM, PD, S, PF, 24>(p, st);
   }
   return hipErrorInvalidValue;
 }
 
-// tile configurations {WM, WN, TN, TM, PD, S} (variants 270 + row): pixels 16 * WM * TM x channels
-// 16 * WN * TN, weights PD column steps ahead, stride S.  Kept from the round-4 sweep of 20 stride-1
-// configurations (profiles/r4lr/tune{1,2,3}.txt, one layer forced at a time in the yolov7 bs-32
-// forward): 4-wave blocks of 80-pixel tiles with the weights three column steps ahead won every layer
-// shape; the 8-wave and 128 / 160-pixel tiles, and two steps of prefetch, lost by 5-20 %.  0: 80 x 128,
-// 1: 80 x 64; 2 / 3: the same with 64-pixel tiles for heights that 5 does not divide.  4: stride 2,
-// 64 x 128.  At stride 2 the same four were correct but slower than the dispatch on the large yolov7
-// stride-2 layers (profiles/r4lr/convbench_s2.txt: 64->128 s2 @320 243 vs 215 us, 256->256 s2 @80 77
-// vs 68: a 9-column, 2*TH+1-row patch per output tile is 4-5 input pixels per output against 2.1 at
-// stride 1) and faster only where the dispatch split K: 256->256 s2 @40 25.4 vs 29.6.  5 / 6: 160-pixel
-// tiles (TH = 10) of 128 / 64 channels (profiles/r4lr/tune_tm10*.txt: 3-9 % on the wide layers).
-// Round 5, stride 2 (profiles/r5_s2/cb_deep_s2.txt, tune_deep_*.txt): 7 = 80 x 128 (5 rows) wins on the
-// w6 12 800-pixel layers with cout >= 384 (512->768 s2 @80 109.1 -> 101.5 us in-network); 8 = 128 x 128
-// (8 rows, PD 2) and 9 = 160 x 64 lost everywhere (VGPR-bound weight prefetch, LDS-read bound) and are
-// kept only as forced variants.
-// Reading the next column step's patch rows before this step's MFMAs (two register sets; across a
-// chunk boundary after the barrier) was no faster on any layer and cost a wave per SIMD
-// (profiles/r4lr/tune_xp.txt): three waves per SIMD already hide the LDS latency.
-#define LR_CFGS(X)                                                                                   \
-  X(0, 1, 4, 2, 5, 3, 1) X(1, 1, 4, 1, 5, 3, 1) X(2, 1, 4, 2, 4, 3, 1) X(3, 1, 4, 1, 4, 3, 1) X(4, 1, 4, 2, 4, 3, 2) \
-  X(5, 1, 4, 2, 10, 2, 1) X(6, 1, 4, 1, 10, 3, 1) X(7, 1, 4, 2, 5, 3, 2) X(8, 1, 4, 2, 8, 2, 2) X(9, 1, 4, 1, 10, 3, 2)
-#define LR_ROW(i, wm, wn, tn, tm, pd, s) {wm, wn, tn, tm, pd, s},
-constexpr int LR_CFG[][6] = {LR_CFGS(LR_ROW)};
-constexpr int LR_NCFG = sizeof(LR_CFG) / sizeof(LR_CFG[0]);
 
 }  // namespace
 
@@ -350,11 +553,69 @@ bool lr_supported(const ConvParams& p, int cfg) {
 hipError_t launch_conv_lr(const ConvParams& p, int cfg, hipStream_t st) {
   if (!lr_supported(p, cfg)) return hipErrorInvalidValue;
   switch (cfg) {
-#define LR_CASE(i, wm, wn, tn, tm, pd, s) \
-  case i: return launch_nch<wm, wn, tn, tm, pd, s>(p, st);
+#define LR_CASE(i, wm, wn, tn, tm, pd, s, pf) \
+  case i: return launch_nch<wm, wn, tn, tm, pd, s, pf>(p, st);
     LR_CFGS(LR_CASE)
 #undef LR_CASE
   }
+  return hipErrorInvalidValue;
+}
+
+static int chain_form(const ChainParams& c) {
+  const int n0 = c.p[0].cin / CK, n1 = c.nl > 1 ? c.p[1].cin / CK : 0;
+  int id = 0, k = 0;
+#define CHAIN_ID(a, b, cc, d) \
+  if (id == 0 && c.cfg0 == a && n0 == b && c.cfg1 == cc && n1 == d) id = k + 1; \
+  ++k;
+  CHAIN_FORMS(CHAIN_ID)
+#undef CHAIN_ID
+  return id - 1;
+}
+
+bool chain_supported(const ChainParams& c) {
+  if (c.nl < 2 || c.nl > CHAIN_MAX || chain_form(c) < 0) return false;
+  for (int l = 0; l < c.nl; ++l) {
+    const ConvParams& p = c.p[l];
+    if (!lr_supported(p, l == 0 ? c.cfg0 : c.cfg1) || p.act != c.p[0].act || p.act < 0 || p.act > 2 ||
+        p.B != c.p[0].B || p.Ho != c.p[0].Ho || p.Wo != c.p[0].Wo)
+      return false;
+    if (l > 0 && (p.x != c.p[l - 1].y || p.xoff != c.p[l - 1].yoff || p.xc != c.p[l - 1].yc || p.cin != c.p[l - 1].cout))
+      return false;
+  }
+  return true;
+}
+
+size_t chain_counter_bytes(const ChainParams& c) {
+  const ChainGeo g = chain_geo(c);
+  return (size_t)(CH_BAND0 + CH_LINE * (g.boff[c.nl - 1] + 1)) * 4;
+}
+
+long chain_tasks(const ChainParams& c) { return chain_geo(c).t0[c.nl]; }
+
+hipError_t launch_conv_chain(const ChainParams& c, hipStream_t st) {
+  if (!chain_supported(c) || !c.ctr) return hipErrorInvalidValue;
+  static const int cus = [] {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        v <= 0)
+      v = 256;
+    return v;
+  }();
+  const ChainGeo g = chain_geo(c);
+  const long total = g.t0[c.nl];
+  const int grid = (int)(total < 3L * cus ? total : 3L * cus);   // 3 blocks per CU at most are resident
+  const int form = chain_form(c), act = c.p[0].act;
+  int k = 0;
+#define CHAIN_CASE(a, b, cc, d)                                                                              \
+  if (form == k) {                                                                                           \
+    if (act == 1) YV7_LAUNCH((conv3x3_chain_kernel<a, b, cc, d, 1>), dim3(grid), dim3(256), 0, st, c);       \
+    else if (act == 2) YV7_LAUNCH((conv3x3_chain_kernel<a, b, cc, d, 2>), dim3(grid), dim3(256), 0, st, c);  \
+    else YV7_LAUNCH((conv3x3_chain_kernel<a, b, cc, d, 0>), dim3(grid), dim3(256), 0, st, c);                \
+    return hipGetLastError();                                                                                \
+  }                                                                                                          \
+  ++k;
+  CHAIN_FORMS(CHAIN_CASE)
+#undef CHAIN_CASE
   return hipErrorInvalidValue;
 }
 

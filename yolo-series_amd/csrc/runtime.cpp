@@ -162,7 +162,7 @@ yv7::ConvParams conv_params(const yv7_plan* p, size_t op, int B, int H, int W) {
   c.M = B * c.Ho * c.Wo;
   c.xbytes = (uint32_t)tensor_bytes(p, ti, B, H, W);
   c.wbytes = (uint32_t)((size_t)((o.cout + 31) / 32 * 32) * c.kpad * es);
-  c.variant = p->op_variant[op];
+  c.variant = p->op_variant[op] == 305 ? 0 : p->op_variant[op];   // 305: a chain start (find_chain)
   if (p->wfrag && p->wf_off[op] >= 0) {
     c.wf = reinterpret_cast<const unsigned char*>(p->wfrag) + p->wf_off[op];
     c.wfbytes = (uint32_t)yv7::frag_bytes(o.cin, o.cout, o.k * o.k);
@@ -177,8 +177,83 @@ struct SplitScratch {
   size_t part_off = 0, part_bytes = 0, cnt_off = 0;
   int cnt_n = 0;
   size_t f8_off = 0, f8_bytes = 0;   // dense e4m3 copy of an FP8 op's input (the largest one)
+  size_t chain_off = 0, chain_bytes = 0;   // ready counters of a chained 3x3 launch (the largest chain)
   size_t end = 0;
 };
+
+// A chain of 3x3 stride-1 fp16 convs starting at op i that the runtime launches as ONE kernel
+// (conv_lr.hip conv3x3_chain_kernel: an ELAN block's 3x3 stack): ops i .. i + n - 1, each reading the
+// previous one's output slice, all of a shape the low-resolution kernel takes.  NOT in the default dispatch:
+// measured slower than the per-layer launches on every yolov7 bs 32 stack it applies to (round 6,
+// profiles/r6_chain/: 20^2 256 x 4 116.8 vs 89.4 us, 40^2 128 x 4 130.0 vs 105.0; bench 7679 / 7710 vs 7847 /
+// 7868 img/s) — each layer's 640 tiles are one round of the chip, so the next layer's tiles find nothing to
+// overlap with, and the queue's dequeues plus the polls cost more than the three kernel boundaries they
+// remove.  Forced per chain with variant 305 on its first op (yv7_set_op_variant; the later ops on 0);
+// YV7_CHAIN=1 chains every eligible stack.  Fills *c (pointers from workspace base wsb, null for a layout
+// query) and returns n (0: no chain here).
+int find_chain(const yv7_plan* p, size_t i, int B, int H, int W, const std::vector<size_t>& off, unsigned char* wsb,
+               yv7::ChainParams* c) {
+  static const int all = [] { const char* e = getenv("YV7_CHAIN"); return e ? atoi(e) : 0; }();
+  static const long max_tasks = [] { const char* e = getenv("YV7_CHAIN_TASKS"); return e ? atol(e) : 1280L; }();
+  if (p->dtype != YV7_DT_F16 || i >= p->ops.size()) return 0;
+  const bool forced = p->op_variant[i] == 305;
+  if (!forced && !all) return 0;
+  const unsigned char* wb = reinterpret_cast<const unsigned char*>(p->weights);
+  auto eligible = [&](size_t j) {
+    const auto& o = p->ops[j];
+    return o.kind == YV7_OP_CONV && !is_f8(o) && o.k == 3 && o.s == 1 && o.pad == 1 && !o.pool &&
+           p->op_variant[j] == (j == i && forced ? 305 : 0) && o.act == p->ops[i].act;
+  };
+  if (!eligible(i)) return 0;
+  size_t n = 1;
+  while (n < (size_t)yv7::CHAIN_MAX && i + n < p->ops.size() && eligible(i + n)) {
+    const auto& a = p->ops[i + n - 1];
+    const auto& b = p->ops[i + n];
+    if (b.src != a.dst || b.src_coff != a.dst_coff || b.cin != a.cout) break;
+    ++n;
+  }
+  // no layer's output may overlap the chain's input slice or another layer's output
+  auto overlap = [](int ta, int ca, int na, int tb, int cb, int nb) { return ta == tb && ca < cb + nb && cb < ca + na; };
+  for (; n >= 2; --n) {
+    bool ok = true;
+    for (size_t j = 0; j < n && ok; ++j) {
+      const auto& oj = p->ops[i + j];
+      if (overlap(oj.dst, oj.dst_coff, oj.cout, p->ops[i].src, p->ops[i].src_coff, p->ops[i].cin)) ok = false;
+      for (size_t k = 0; k < j && ok; ++k) {
+        const auto& ok_ = p->ops[i + k];
+        if (overlap(oj.dst, oj.dst_coff, oj.cout, ok_.dst, ok_.dst_coff, ok_.cout)) ok = false;
+      }
+    }
+    if (!ok) continue;
+    std::memset(c, 0, sizeof(*c));
+    c->nl = (int)n;
+    for (size_t j = 0; j < n && ok; ++j) {
+      const auto& o = p->ops[i + j];
+      yv7::ConvParams& q = c->p[j];
+      q = conv_params(p, i + j, B, H, W);
+      const auto& to = p->tensors[o.dst];
+      q.x = wsb + off[o.src];
+      q.w = wb + o.w_off;
+      q.bias = reinterpret_cast<const float*>(wb + o.b_off);
+      q.zero = p->zero;
+      q.y = wsb + off[o.dst];
+      q.yc = to.channels;
+      q.yoff = o.dst_coff;
+      q.variant = 0;
+      if (q.Ho != (H >> to.shift) || q.Wo != (W >> to.shift)) ok = false;
+      int cfg = yv7::lr_default_cfg(q);
+      if (cfg == 0 || cfg == 2) ++cfg;   // 128-channel tiles -> 64-channel (conv_lr.hip CHAIN_FORMS)
+      if (cfg < 0 || (j > 1 && cfg != c->cfg1)) ok = false;
+      if (j == 0) c->cfg0 = cfg;
+      if (j == 1) c->cfg1 = cfg;
+    }
+    if (!ok || !yv7::chain_supported(*c)) continue;
+    // (YV7_CHAIN=1: only where a layer has few tiles, its ramp and tail dominating)
+    if (!forced && yv7::chain_tasks(*c) > max_tasks * (long)n) return 0;
+    return (int)n;
+  }
+  return 0;
+}
 
 SplitScratch split_scratch(const yv7_plan* p, int B, int H, int W, size_t tensors_end) {
   SplitScratch s;
@@ -198,7 +273,14 @@ SplitScratch split_scratch(const yv7_plan* p, int B, int H, int W, size_t tensor
   s.part_off = tensors_end;
   s.cnt_off = align256(s.part_off + s.part_bytes);
   s.f8_off = align256(s.cnt_off + (size_t)s.cnt_n * 4);
-  s.end = align256(s.f8_off + s.f8_bytes);
+  s.chain_off = align256(s.f8_off + s.f8_bytes);
+  if (p->dtype == YV7_DT_F16) {
+    std::vector<size_t> zero_off(p->tensors.size(), 0);
+    yv7::ChainParams c;
+    for (size_t i = 0; i < p->ops.size(); ++i)
+      if (find_chain(p, i, B, H, W, zero_off, nullptr, &c)) s.chain_bytes = std::max(s.chain_bytes, yv7::chain_counter_bytes(c));
+  }
+  s.end = align256(s.chain_off + s.chain_bytes);
   return s;
 }
 
@@ -422,8 +504,9 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (kind == YV7_OP_DETECT) return v == 92 || v == 94 || v == 97 || v == 99;
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15 || v == 17) return true;
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
+  if (v == 305) return o.k == 3 && o.s == 1;   // the chained launch of the 3x3 stack starting here (find_chain)
   return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
-         (v >= 270 && v <= 288) || (v >= 290 && v <= 295) || v == 302 || v == 303;
+         (v >= 270 && v <= 288) || (v >= 290 && v <= 295) || v == 302 || v == 303 || (v >= 306 && v <= 309);
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {
@@ -613,6 +696,18 @@ static int forward_impl(yv7_plan* p, const void* x, int x_dtype, int B, int H, i
             f.act = o.act;
             e = yv7::launch_conv_f8(f, st);
             break;
+          }
+          // An ELAN block's 3x3 stack as ONE chained launch (find_chain, conv_lr.hip conv3x3_chain_kernel);
+          // the later ops of the chain record no time of their own.
+          {
+            yv7::ChainParams ch;
+            const int n = find_chain(p, i, B, H, W, off, wsb, &ch);
+            if (n) {
+              ch.ctr = reinterpret_cast<int*>(wsb + scr.chain_off);
+              e = yv7::launch_conv_chain(ch, st);
+              fused_until = i + n;
+              break;
+            }
           }
           // The MP block's two readers of one tensor (cfg/deploy/yolov7.yaml: `MP -> 1x1` and `1x1`,
           // adjacent ops here: the pooled one is the fp16 plan's pool = 2 op) as ONE register-streamed

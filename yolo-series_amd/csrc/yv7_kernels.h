@@ -211,6 +211,26 @@ bool hring_supported(const ConvParams& p);
 // low-resolution 3x3 (conv_lr.hip): cfg 0-4 = tile shape; weights from ConvParams::wf
 bool lr_supported(const ConvParams& p, int cfg);
 hipError_t launch_conv_lr(const ConvParams& p, int cfg, hipStream_t st);
+// The low-resolution configuration the default fp16 dispatch gives a 3x3 stride-1 layer (conv_f16.hip
+// launch_conv_f16), or -1 when another kernel takes it.
+int lr_default_cfg(const ConvParams& p);
+// A chain of 3x3 stride-1 convs at one resolution, each reading the previous one's output slice (an ELAN
+// block's 3x3 stack, cfg/deploy/yolov7.yaml:65-68, 84-87, 98-101, 113-116, 128-131) as ONE launch of
+// conv_lr.hip's tile body (conv3x3_chain_kernel): layer l + 1's tiles start as soon as the rows of layer l
+// they read are done (per image group and row band ready counters), instead of after layer l's last tile.
+constexpr int CHAIN_MAX = 4;
+struct ChainParams {
+  ConvParams p[CHAIN_MAX];   // layer l: its own kernel parameters (p[l + 1].x / xoff = p[l].y / yoff)
+  int nl;                    // layers, 2 .. CHAIN_MAX
+  int cfg0, cfg1;            // low-resolution configuration of layer 0 and of layers 1 .. nl - 1
+  int* ctr;                  // chain_counter_bytes() of workspace scratch, zeroed once, re-armed by the kernel
+};
+// the chain's launch form exists (configurations, widths, activation) and its geometry is consistent;
+// ctr may be null here (a layout query)
+bool chain_supported(const ChainParams& c);
+size_t chain_counter_bytes(const ChainParams& c);
+long chain_tasks(const ChainParams& c);   // tiles of all layers
+hipError_t launch_conv_chain(const ChainParams& c, hipStream_t st);
 size_t frag_bytes(int cin, int cout, int taps);
 hipError_t pack_frag(const void* w, int kpad, int cin, int cout, int taps, void* out, hipStream_t st);
 hipError_t launch_conv_hring(const ConvParams& p, int cus, hipStream_t st);
