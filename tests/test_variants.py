@@ -10,8 +10,7 @@ splits (1CS: configuration C, S splits; the split-K hand-off of splitk_reduce), 
 (201-206), the 8-phase rings (231: 256 x 256, 232: 256 x 128), the weight-stationary 1x1 rings (234-236,
 and 239: N-split), the column-group 3x3 halo ring (262), the
 low-resolution 3x3 kernel (270-273: 80 / 64-pixel tiles of 4 images x 4 columns, 128 / 64 channels;
-274 / 277-279: stride 2; 275 / 276: 160-pixel tiles; 306-309: 270 / 271 / 273 / 276 with the patch two chunks
-ahead), the register-weight 3x3 kernel (280-284: stride 2,
+274 / 277-279: stride 2; 275 / 276: 160-pixel tiles), the register-weight 3x3 kernel (280-284: stride 2,
 285-288: stride 1; cin 64 / 128, 2-5 ring slots, 2-8-row tiles, with and without the stagger), the register-weight 1x1 kernel (290-295: cin 128 / 256 / 512, with and
 without the stagger; 302 / 303: cin 256 with 128-channel N slices) and
 the alternative Detect heads (92, 97, and 99: the 64 x 256 ring that was the default before the
@@ -33,7 +32,7 @@ CONV_VARIANTS = [1, 2, 4, 5, 6, 7, 8, 10, 11, 15, 17,
                  100, 102, 104, 110, 112, 114, 120, 122, 124, 130, 132, 134, 140, 142, 144, 150, 152, 154,
                  201, 202, 203, 204, 205, 206, 231, 232, 234, 235, 236, 239, 262, 270, 271, 272, 273, 274, 275, 276,
                  277, 278, 279, 280, 281, 282, 283, 284, 285, 286, 287, 288, 290, 291, 292, 293,
-                 294, 295, 302, 303, 306, 307, 308, 309]
+                 294, 295, 302, 303]
 DET_VARIANTS = [92, 94, 97, 99]
 
 
@@ -115,7 +114,7 @@ def test_fragment_kernels_ragged(B):
     convs = [i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV]
     lines = []
     for v in [0, 270, 271, 272, 273, 274, 275, 276, 277, 278, 279, 280, 281, 282, 283, 284, 285, 286, 287, 288,
-              290, 291, 292, 293, 294, 295, 302, 303, 306, 307, 308, 309]:
+              290, 291, 292, 293, 294, 295, 302, 303]:
         for i in convs:
             plan.set_op_variant(i, v)
         if v in W1_CIN:

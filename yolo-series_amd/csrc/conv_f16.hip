@@ -2300,8 +2300,6 @@ hipError_t launch_conv_f16(const ConvParams& p, bool det, hipStream_t st) {
     return launch_conv_hring(p, device_cus(), st);
   // the low-resolution 3x3 kernel (conv_lr.hip): 270 + tile configuration
   if (!det && variant >= 270 && variant <= 279 && lr_supported(p, variant - 270)) return launch_conv_lr(p, variant - 270, st);
-  // its configurations 10-13 (the patch two chunks ahead): 306-309
-  if (!det && variant >= 306 && variant <= 309 && lr_supported(p, variant - 296)) return launch_conv_lr(p, variant - 296, st);
   // the register-weight stride-2 kernel (conv_s2.hip): 280 + tile configuration
   if (!det && variant >= 280 && variant <= 288 && s2_supported(p, variant - 280))
     return launch_conv_s2(p, variant - 280, device_cus(), st);

@@ -72,15 +72,16 @@ struct LrGeo {
 // Reading the next column step's patch rows before this step's MFMAs (two register sets; across a
 // chunk boundary after the barrier) was no faster on any layer and cost a wave per SIMD
 // (profiles/r4lr/tune_xp.txt): three waves per SIMD already hide the LDS latency.
-// Round 6 (PF = 2, rows 10-13, variants 306-309): rows 0 / 1 / 3 / 6 with the input patch loaded two
-// chunks ahead (two register sets) instead of one — at 20^2 / 40^2 a layer's ~640 tiles leave 2-3 waves per
-// SIMD, too few to hide a chunk's HBM / MALL latency behind one chunk of MFMAs (profiles/r6_diag_batch/:
-// these layers run 17-37 % faster per image at bs 64 / 128).
+// Round 6: the input patch loaded two chunks ahead (PF = 2: two register sets) on rows 0 / 1 / 3 / 6 was
+// no faster on any yolov7 bs-32 layer it could take (one layer forced at a time, profiles/r6_lr_pf2/tune.txt:
+// 256->256 @20 22.7 -> 22.8 us, 128->128 @40 21.9 -> 22.3, 512->512 @20 59.2 -> 62.2): the patch's HBM / MALL
+// latency is not what these layers wait on; nor did the weights four to seven column steps ahead (PD 4-7
+// on rows 0 / 1 / 6, profiles/r6_lr_pd/tune.txt: 22.7 -> 23.5, 61.1 -> 65.8, 38.8 -> 41.6 us).  The PF column
+// stays (1 everywhere).
 #define LR_CFGS(X)                                                                                   \
   X(0, 1, 4, 2, 5, 3, 1, 1) X(1, 1, 4, 1, 5, 3, 1, 1) X(2, 1, 4, 2, 4, 3, 1, 1) X(3, 1, 4, 1, 4, 3, 1, 1)          \
   X(4, 1, 4, 2, 4, 3, 2, 1) X(5, 1, 4, 2, 10, 2, 1, 1) X(6, 1, 4, 1, 10, 3, 1, 1) X(7, 1, 4, 2, 5, 3, 2, 1)        \
-  X(8, 1, 4, 2, 8, 2, 2, 1) X(9, 1, 4, 1, 10, 3, 2, 1) X(10, 1, 4, 2, 5, 3, 1, 2) X(11, 1, 4, 1, 5, 3, 1, 2)      \
-  X(12, 1, 4, 1, 4, 3, 1, 2) X(13, 1, 4, 1, 10, 3, 1, 2)
+  X(8, 1, 4, 2, 8, 2, 2, 1) X(9, 1, 4, 1, 10, 3, 2, 1)
 #define LR_ROW(i, wm, wn, tn, tm, pd, s, pf) {wm, wn, tn, tm, pd, s, pf},
 constexpr int LR_CFG[][7] = {LR_CFGS(LR_ROW)};
 constexpr int LR_NCFG = sizeof(LR_CFG) / sizeof(LR_CFG[0]);

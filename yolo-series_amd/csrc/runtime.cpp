@@ -506,7 +506,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
   if (v == 305) return o.k == 3 && o.s == 1;   // the chained launch of the 3x3 stack starting here (find_chain)
   return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
-         (v >= 270 && v <= 288) || (v >= 290 && v <= 295) || v == 302 || v == 303 || (v >= 306 && v <= 309);
+         (v >= 270 && v <= 288) || (v >= 290 && v <= 295) || v == 302 || v == 303;
 }
 
 int yv7_set_op_variant(yv7_plan* p, int op, int variant) {
