@@ -35,7 +35,7 @@ import torch.distributed as dist  # noqa: E402
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 # HBM bytes per conv launch from PMC counters of this same workload (scripts/pmc_traffic.sh: separate
 # FETCH_SIZE / WRITE_SIZE rocprofv3 passes; scripts/pmc_traffic.py: x2 FETCH correction for gfx950)
-PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r5_pmc_traffic.json')   # per kernel (scripts/pmc_traffic_kernels.py)
+PMC_TRAFFIC = os.path.join(ROOT, 'profiles', 'r6_pmc_traffic.json')   # per kernel (scripts/pmc_traffic_kernels.py)
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16 MFMA
 
 
