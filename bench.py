@@ -101,6 +101,9 @@ def plumbing(a):
     """The N > 1 data path on CPU ranks (gloo): the same yv7.dist calls the GPU ranks make, minus the
     kernels.  Prints one JSON line with the world size the process group saw."""
     from yv7 import dist as ydist
+    sys.stdout.flush()
+    json_fd = os.dup(1)   # stdout: the JSON line only (gloo announces its connections on fd 1)
+    os.dup2(2, 1)
     ydist.init('gloo')
     world, rank = dist.get_world_size(), dist.get_rank()
     if world != a.gpus:
@@ -159,14 +162,14 @@ def plumbing(a):
     pl = [torch.zeros_like(per) for _ in range(world)]
     dist.all_gather(pl, per)
     if rank == 0:
-        print(json.dumps({'plumbing': True, 'dtype': a.dtype, 'n_gpus': world, 'world_size_seen': world, 'backend': 'gloo',
+        os.write(json_fd, (json.dumps({'plumbing': True, 'dtype': a.dtype, 'n_gpus': world, 'world_size_seen': world, 'backend': 'gloo',
                           'rccl_world_size': world, 'model': a.model,
                           'weights_broadcast_bytes': int(blob.numel()), 'global_batch': gbatch,
                           'all_ranks_ok': bool(flags.item()),
                           'shards': [[int(v[2]), int(v[3])] for v in pl],
                           'gathered_in_global_order': [bool(v[4]) for v in pl],
                           'allgather_us_per_batch': [round(float(v[0]), 1) for v in pl],
-                          'per_rank_world_size_seen': [int(v[1]) for v in pl]}), flush=True)
+                          'per_rank_world_size_seen': [int(v[1]) for v in pl]}) + '\n').encode())
     dist.barrier()
     wd.stop()
     dist.destroy_process_group()
@@ -286,7 +289,13 @@ def main(argv=None):
     torch.cuda.set_device(local)
     from yv7 import dist as ydist
     wd = None
+    json_fd = None
     if distributed:
+        # stdout carries exactly ONE line, the JSON result: RCCL prints its version banner to fd 1 when its
+        # first communicator comes up, so every other write to fd 1 goes to stderr from here on
+        sys.stdout.flush()
+        json_fd = os.dup(1)
+        os.dup2(2, 1)
         # process-group timeout + a host-side progress watchdog: a dead or hung peer ends this rank with a
         # non-zero exit naming the rank, phase and batch, not a wait for the outer kill
         ydist.init('nccl', torch.device(f'cuda:{local}'))
@@ -695,7 +704,10 @@ def main(argv=None):
                                                parity_frames=a.map_frames)
             if 'map_parity' in res['cpu_baseline']:
                 res['map50_parity'] = res['cpu_baseline']['map_parity']['map50']
-        print(json.dumps(res), flush=True)
+        if json_fd is None:
+            print(json.dumps(res), flush=True)
+        else:
+            os.write(json_fd, (json.dumps(res) + '\n').encode())
     if distributed:
         beat('final barrier')
         dist.barrier()

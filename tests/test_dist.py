@@ -265,6 +265,8 @@ def test_bench_launcher_starts_ranks():
                           '--model', 'yolov7-tiny', '--batch', '3'], capture_output=True, text=True, env=env,
                          timeout=600)
     assert out.returncode == 0, out.stderr[-3000:]
+    # stdout is exactly the one JSON line (the backend's own chatter goes to stderr: bench.py dup2)
+    assert len(out.stdout.strip().splitlines()) == 1, out.stdout
     lines = [json.loads(l) for l in out.stdout.splitlines() if l.startswith('{')]
     assert len(lines) == 1, out.stdout
     r = lines[0]
