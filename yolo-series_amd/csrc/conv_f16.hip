@@ -1112,6 +1112,19 @@ __device__ __forceinline__ bool splitk_reduce(const ConvParams& p, unsigned char
   return true;
 }
 
+// vmcnt before ring step kt: stage kt landed, the min(MAXN, ahead) stages issued after it (PER DMA
+// instructions each) may stay in flight — an immediate per case
+template <int PER, int MAXN>
+__device__ __forceinline__ void ring_wait(int ahead) {
+  if constexpr (MAXN <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    static_assert(MAXN * PER <= 63, "vmcnt range");
+    if (ahead >= MAXN) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MAXN * PER) : "memory");
+    else ring_wait<PER, MAXN - 1>(ahead);
+  }
+}
+
 // ---------------------------------------------------------------------------------------------
 // 8-wave LDS-DMA ring (wide layers).
 //  * 512 threads = 8 waves (2 per SIMD, so one wave's fragment reads hide under the other's MFMAs),
@@ -1203,9 +1216,7 @@ __global__ __launch_bounds__(64 * WM * WN, (STAGES * (BM + BN) * 128 <= 80 * 102
   for (int kt = 0; kt < nk; ++kt) {
     // stage kt must have landed; the (at most STAGES-2) stages issued after it may stay in flight
     const int ahead = nk - 1 - kt;
-    if (STAGES >= 4 && ahead >= 2) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * PER) : "memory");
-    else if (STAGES >= 3 && ahead >= 1) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    ring_wait<PER, STAGES - 2>(ahead);
     __builtin_amdgcn_s_barrier();
     if (kt + STAGES - 1 < nk) {
       int fs = slot + STAGES - 1;
@@ -2160,9 +2171,13 @@ hipError_t launch_t(const ConvParams& p, hipStream_t st) {
 namespace {
 
 // Ring-kernel configurations the split-K dispatch chooses from: tile BM x BN, waves, LDS stages.
-enum RingCfg { R256x256, R256x128, R128x128s3, R128x128s2, R128x64, R256x64, NCFG };
-constexpr int cfg_bm[NCFG] = {256, 256, 128, 128, 128, 256};
-constexpr int cfg_bn[NCFG] = {256, 128, 128, 128, 64, 64};
+// Round 6: deep rings for the low-resolution deep-K layers (whose 2-stage ring waits out an L2 round trip
+// every K step): 128 x 128 with 8 waves and 5 stages (3 in flight), 128 x 64 with 8 waves and 6 stages
+// (4 in flight), 128 x 128 with 4 waves and 5 stages — one block per CU (160 / 144 KiB of LDS).
+enum RingCfg { R256x256, R256x128, R128x128s3, R128x128s2, R128x64, R256x64, R128x128w8s5, R128x64w8s6, R128x128s5,
+               NCFG };
+constexpr int cfg_bm[NCFG] = {256, 256, 128, 128, 128, 256, 128, 128, 128};
+constexpr int cfg_bn[NCFG] = {256, 128, 128, 128, 64, 64, 128, 64, 128};
 
 struct Choice {
   int cfg = -1;   // ring configuration, -1 = the legacy dispatch (halo / tile kernels / old variants)
@@ -2238,6 +2253,9 @@ hipError_t launch_choice(const ConvParams& p, const Choice& c, bool one, hipStre
     case R128x128s2: return launch_ring_s<128, 128, 2, 2, 2>(p, one, c.S, st);
     case R128x64: return launch_ring_s<128, 64, 2, 2, 3>(p, one, c.S, st);
     case R256x64: return launch_ring_s<256, 64, 4, 2, 3>(p, one, c.S, st);
+    case R128x128w8s5: return launch_ring_s<128, 128, 2, 4, 5>(p, one, c.S, st);
+    case R128x64w8s6: return launch_ring_s<128, 64, 2, 4, 6>(p, one, c.S, st);
+    case R128x128s5: return launch_ring_s<128, 128, 2, 2, 5>(p, one, c.S, st);
   }
   return hipErrorInvalidValue;
 }
