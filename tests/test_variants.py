@@ -140,7 +140,7 @@ def test_variant_api_rejects_hooks():
     m = fresh_model('yolov7-tiny').to(DEV).half()
     plan = m.plan()
     conv = next(i for i, o in enumerate(plan.graph.ops) if o['kind'] == L.OP_CONV)
-    for v in (12, 13, 14, 16, 18, 19, 90, 91, 93, 94, 298, 190, 105, 211, 221, 233, 237, 238, 240, 241,
+    for v in (12, 13, 14, 16, 18, 19, 90, 91, 93, 94, 298, 160, 190, 105, 211, 221, 233, 237, 238, 240, 241,
               248, 255, 259, 260, 261, 263, 289, 296, 299, 300, 301, 304, 911):
         with pytest.raises(RuntimeError):
             plan.set_op_variant(conv, v)

@@ -2171,13 +2171,11 @@ hipError_t launch_t(const ConvParams& p, hipStream_t st) {
 namespace {
 
 // Ring-kernel configurations the split-K dispatch chooses from: tile BM x BN, waves, LDS stages.
-// Round 6: deep rings for the low-resolution deep-K layers (whose 2-stage ring waits out an L2 round trip
-// every K step): 128 x 128 with 8 waves and 5 stages (3 in flight), 128 x 64 with 8 waves and 6 stages
-// (4 in flight), 128 x 128 with 4 waves and 5 stages — one block per CU (160 / 144 KiB of LDS).
-enum RingCfg { R256x256, R256x128, R128x128s3, R128x128s2, R128x64, R256x64, R128x128w8s5, R128x64w8s6, R128x128s5,
-               NCFG };
-constexpr int cfg_bm[NCFG] = {256, 256, 128, 128, 128, 256, 128, 128, 128};
-constexpr int cfg_bn[NCFG] = {256, 128, 128, 128, 64, 64, 128, 64, 128};
+// (Round 6: 128 x 128 / 128 x 64 rings with 5-6 stages, 3-4 in flight, one block per CU, were slower on
+// every 20^2 / 40^2 deep-K 1x1 layer: 1024->512 @20 25.9 -> 31.7 us, profiles/r6_ring_deep/tune.txt.)
+enum RingCfg { R256x256, R256x128, R128x128s3, R128x128s2, R128x64, R256x64, NCFG };
+constexpr int cfg_bm[NCFG] = {256, 256, 128, 128, 128, 256};
+constexpr int cfg_bn[NCFG] = {256, 128, 128, 128, 64, 64};
 
 struct Choice {
   int cfg = -1;   // ring configuration, -1 = the legacy dispatch (halo / tile kernels / old variants)
@@ -2253,9 +2251,6 @@ hipError_t launch_choice(const ConvParams& p, const Choice& c, bool one, hipStre
     case R128x128s2: return launch_ring_s<128, 128, 2, 2, 2>(p, one, c.S, st);
     case R128x64: return launch_ring_s<128, 64, 2, 2, 3>(p, one, c.S, st);
     case R256x64: return launch_ring_s<256, 64, 4, 2, 3>(p, one, c.S, st);
-    case R128x128w8s5: return launch_ring_s<128, 128, 2, 4, 5>(p, one, c.S, st);
-    case R128x64w8s6: return launch_ring_s<128, 64, 2, 4, 6>(p, one, c.S, st);
-    case R128x128s5: return launch_ring_s<128, 128, 2, 2, 5>(p, one, c.S, st);
   }
   return hipErrorInvalidValue;
 }

@@ -503,7 +503,7 @@ static bool variant_allowed(const yv7_op_desc& o, int v) {
   if (is_f8(o)) return v == 81 || v == 82;   // fp8 1x1: staged quantize pass / fused quantization
   if (kind == YV7_OP_DETECT) return v == 92 || v == 94 || v == 97 || v == 99;
   if (v == 1 || v == 2 || (v >= 4 && v <= 8) || v == 10 || v == 11 || v == 15 || v == 17) return true;
-  if (v >= 100 && v < 190 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
+  if (v >= 100 && v < 160 && v % 10 <= 4) return true;   // ring configuration (v - 100) / 10, v % 10 K-splits
   if (v == 305) return o.k == 3 && o.s == 1;   // the chained launch of the 3x3 stack starting here (find_chain)
   return (v >= 201 && v <= 206) || v == 231 || v == 232 || (v >= 234 && v <= 236) || v == 239 || v == 262 ||
          (v >= 270 && v <= 288) || (v >= 290 && v <= 295) || v == 302 || v == 303;
