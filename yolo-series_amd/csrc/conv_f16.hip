@@ -658,14 +658,23 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
 // step, each feeding 2 MFMAs).  Epilogue and row records as conv_det_pring_kernel (det_tail_fixed; the
 // same sigmoid and decode: bit-identical z and records).
 // HOOK (detbench only, variant 91; the ABI never accepts it): 1 = no pixel DMA (stale LDS operands)
-template <int NCH, int HOOK = 0>
+// D (round 6): pixel stages in flight ahead of the one being read.  D = 0 is the round-5 schedule (a
+// two-slot ring: the K step's stage issued one step ahead, plus the next tile's second stage before the
+// epilogue).  D > 0: a (D + 1)-slot ring, one stage issued per K step D steps ahead, so at K = 256 (4 steps)
+// the whole next tile's pixels are in flight during this tile's epilogue instead of being waited for inside
+// its K loop.  Stage s is read at global step s; the stores of the epilogue between two tiles are younger
+// than the stages issued before it, so the counted wait at step k of a tile allows D - 1 younger stages,
+// plus the previous epilogue's nst stores while those stages were issued before it (k < D, tile > 0).
+template <int NCH, int HOOK = 0, int D = 0>
 __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p) {
   constexpr int BM = 64, BN = 256, NTH = 512, TM = 4, TN = 2, NK = NCH / 2;
   constexpr int PER = HOOK == 1 ? 0 : 1;           // one A piece per wave per stage
   constexpr int STAGE = BM * ROWB;                 // 8 KiB
-  constexpr int RING = 2 * STAGE;
+  constexpr int R = D > 0 ? D + 1 : 2;             // ring slots
+  constexpr int RING = R * STAGE;
   constexpr int LDS = RING + det_lds(BM, BN);
   static_assert(LDS <= 160 * 1024, "LDS budget");
+  static_assert(D == 0 || ((D - 1) * PER + 10 <= 63 && D <= NK), "counted waits");
   constexpr int NO = 85, NA = 3;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
   unsigned char* es = smem + RING;                 // zs + row table
@@ -699,13 +708,13 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
     const int b = m / hw, cell = m - b * hw, ho = cell / p.Wo, wo = cell - ho * p.Wo;
     return (uint32_t)((pix_index(b, ho, wo, p.H, p.W) * p.xc + p.xoff + c8 * 8) * 2);
   };
-  // stage q = (tile it, K step k) into slot q & 1
-  int i_it = 0, i_k = 0, i_q = 0;
+  // stage q = (tile it, K step k) into slot q % R
+  int i_it = 0, i_k = 0, i_slot = 0;
   uint32_t i_aoff = a_off(0);
   auto issue = [&]() __attribute__((always_inline)) {
-    if constexpr (HOOK != 1) dma16(xr, smem + (i_q & 1) * STAGE + wave * 8 * ROWB, i_aoff, (uint32_t)i_k * BKE * 2);
+    if constexpr (HOOK != 1) dma16(xr, smem + i_slot * STAGE + wave * 8 * ROWB, i_aoff, (uint32_t)i_k * BKE * 2);
     asm volatile("" ::: "memory");
-    ++i_q;
+    if (++i_slot == R) i_slot = 0;
     if (++i_k == NK) {
       i_k = 0;
       ++i_it;
@@ -733,8 +742,9 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
     }
   if (tid < 8) det_tab_ptrs<BM, BN>(es).anc[tid] = p.anchor[tid];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // weights, bias, anchors
-  issue();
-  issue();
+#pragma unroll
+  for (int d = 0; d < (D > 0 ? D : 2); ++d) issue();
+  int r_slot = 0;   // the slot of the stage the next K step reads
   for (int it = 0; it < ntl; ++it) {
     const int m0 = tw.at(it) * BM;
     f4 acc[TN][TM];
@@ -744,22 +754,29 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
       for (int i = 0; i < TM; ++i) acc[j][i] = bv[j];
 #pragma unroll
     for (int k = 0; k < NK; ++k) {
-      // stage (it, k) landed: younger are stage (it, 1) and the previous epilogue's stores at k = 0, the
-      // previous epilogue's stores at k = 1 (both stages of a tile start are issued before them)
-      if (k == 0) {
-        if (it > 0 && nst == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 10) : "memory");
-        else if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 8) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
-      } else if (k == 1 && it > 0) {
-        if (nst == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-        else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      if constexpr (D == 0) {
+        // stage (it, k) landed: younger are stage (it, 1) and the previous epilogue's stores at k = 0, the
+        // previous epilogue's stores at k = 1 (both stages of a tile start are issued before them)
+        if (k == 0) {
+          if (it > 0 && nst == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 10) : "memory");
+          else if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 8) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
+        } else if (k == 1 && it > 0) {
+          if (nst == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+        } else {
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        }
       } else {
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (k >= D || it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * PER) : "memory");
+        else if (nst == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * PER + 10) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * PER + 8) : "memory");
       }
       __builtin_amdgcn_s_barrier();
-      if (k >= 1) issue();              // stage (it, k + 1) or the next tile's first stage
+      if (D > 0 || k >= 1) issue();     // D > 0: stage s + D; D = 0: stage (it, k + 1) or the next tile's first
       if (k == 0) det_table<BM, BN, NTH, false>(p, es, m0, tid);   // read after the K loop's last barrier
-      const unsigned char* As = smem + ((it * NK + k) & 1) * STAGE;
+      const unsigned char* As = smem + r_slot * STAGE;
+      if (++r_slot == R) r_slot = 0;
 #pragma unroll
       for (int s2 = 0; s2 < 2; ++s2) {
         const int ch = s2 * 4 + g;
@@ -779,10 +796,10 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
         __builtin_amdgcn_s_setprio(0);
       }
     }
-    // epilogue: ring reads done -> the next tile's stage (it + 1, 1) into the free slot
+    // epilogue: ring reads done (D = 0: -> the next tile's stage (it + 1, 1) into the free slot)
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
-    issue();
+    if constexpr (D == 0) issue();
     // staging: the sigmoid of every logit into zs (z's layout); the box columns are decoded in
     // det_tail_fixed
     float* zs = reinterpret_cast<float*>(es);
@@ -834,8 +851,17 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
       else YV7_LAUNCH((conv_det_rw_kernel<16, 1>), dim3(grid), dim3(512), 0, st, p);
       return hipGetLastError();
     }
-    if (p.kpad == 256) YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
-    else YV7_LAUNCH(conv_det_rw_kernel<16>, dim3(grid), dim3(512), 0, st, p);
+    // YV7_DET_RWD: pixel stages in flight (conv_det_rw_kernel's D; 0 = the round-5 two-slot schedule)
+    static const int rwd = [] { const char* e = getenv("YV7_DET_RWD"); return e ? atoi(e) : 4; }();
+    if (p.kpad == 256) {
+      if (rwd == 4) YV7_LAUNCH((conv_det_rw_kernel<8, 0, 4>), dim3(grid), dim3(512), 0, st, p);
+      else if (rwd == 3) YV7_LAUNCH((conv_det_rw_kernel<8, 0, 3>), dim3(grid), dim3(512), 0, st, p);
+      else YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
+    } else {
+      if (rwd == 4) YV7_LAUNCH((conv_det_rw_kernel<16, 0, 4>), dim3(grid), dim3(512), 0, st, p);
+      else if (rwd == 3) YV7_LAUNCH((conv_det_rw_kernel<16, 0, 3>), dim3(grid), dim3(512), 0, st, p);
+      else YV7_LAUNCH(conv_det_rw_kernel<16>, dim3(grid), dim3(512), 0, st, p);
+    }
     return hipGetLastError();
   }
   if (p.variant == 98) YV7_LAUNCH(conv_det_pring_kernel<1>, dim3(grid), dim3(512), 0, st, p);
