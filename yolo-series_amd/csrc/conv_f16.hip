@@ -854,13 +854,14 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
     // YV7_DET_RWD: pixel stages in flight (conv_det_rw_kernel's D; 0 = the round-5 two-slot schedule)
     static const int rwd = [] { const char* e = getenv("YV7_DET_RWD"); return e ? atoi(e) : 4; }();
     if (p.kpad == 256) {
-      if (rwd == 4) YV7_LAUNCH((conv_det_rw_kernel<8, 0, 4>), dim3(grid), dim3(512), 0, st, p);
-      else if (rwd == 3) YV7_LAUNCH((conv_det_rw_kernel<8, 0, 3>), dim3(grid), dim3(512), 0, st, p);
-      else YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
-    } else {
-      if (rwd == 4) YV7_LAUNCH((conv_det_rw_kernel<16, 0, 4>), dim3(grid), dim3(512), 0, st, p);
-      else if (rwd == 3) YV7_LAUNCH((conv_det_rw_kernel<16, 0, 3>), dim3(grid), dim3(512), 0, st, p);
-      else YV7_LAUNCH(conv_det_rw_kernel<16>, dim3(grid), dim3(512), 0, st, p);
+      if (rwd == 0) YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
+      else YV7_LAUNCH((conv_det_rw_kernel<8, 0, 4>), dim3(grid), dim3(512), 0, st, p);
+    } else {   // K = 512: 8 K steps, so up to 8 stages may run ahead (YV7_DET_RWD8: 4 / 6 / 8)
+      static const int rwd8 = [] { const char* e = getenv("YV7_DET_RWD8"); return e ? atoi(e) : 4; }();
+      if (rwd == 0) YV7_LAUNCH(conv_det_rw_kernel<16>, dim3(grid), dim3(512), 0, st, p);
+      else if (rwd8 == 8) YV7_LAUNCH((conv_det_rw_kernel<16, 0, 8>), dim3(grid), dim3(512), 0, st, p);
+      else if (rwd8 == 6) YV7_LAUNCH((conv_det_rw_kernel<16, 0, 6>), dim3(grid), dim3(512), 0, st, p);
+      else YV7_LAUNCH((conv_det_rw_kernel<16, 0, 4>), dim3(grid), dim3(512), 0, st, p);
     }
     return hipGetLastError();
   }
