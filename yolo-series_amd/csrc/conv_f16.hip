@@ -481,6 +481,19 @@ __device__ __forceinline__ void det_tail_fixed(const ConvParams& p, unsigned cha
   }
 }
 
+// vmcnt before ring step kt: stage kt landed, the min(MAXN, ahead) stages issued after it (PER DMA
+// instructions each) may stay in flight — an immediate per case
+template <int PER, int MAXN>
+__device__ __forceinline__ void ring_wait(int ahead) {
+  if constexpr (MAXN <= 0) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else {
+    static_assert(MAXN * PER <= 63, "vmcnt range");
+    if (ahead >= MAXN) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MAXN * PER) : "memory");
+    else ring_wait<PER, MAXN - 1>(ahead);
+  }
+}
+
 template <int HOOK = 0>
 __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams p) {
   constexpr int BM = 64, BN = 256, WM = 2, WN = 4, NW = 8, NTH = 512;
@@ -644,6 +657,129 @@ __global__ __launch_bounds__(512, 1) void conv_det_pring_kernel(const ConvParams
     const auto br = make_rsrc(p.best ? p.best + (size_t)zb * 4 : p.z, 0x7fffffffu);
     if constexpr (HOOK < 2) det_tail_fixed<BM, NTH>(p, es, tid, zr, br, zb);
   }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+}
+
+// One-tile Detect head (round 6): where a level has at most one 64-pixel tile per CU (yolov7 bs 32's P5 head,
+// 1024 -> 255 @20: 200 tiles), every block of the persistent head runs ONE tile, and its two-slot ring waits out
+// an L2 round trip at each of the 16 K steps (PMC: 65 % of the wave cycles waiting, profiles/r5_pmc_kernels/).
+// With no next tile to prefetch, the z staging image needs no room of its own during the K loop: four 40 KiB
+// stages (three in flight) fill the LDS, and the staging image + row table reuse it after the loop.  Same
+// arithmetic as conv_det_pring_kernel (bit-identical z and row records).
+__global__ __launch_bounds__(512, 1) void conv_det_1tile_kernel(const ConvParams p) {
+  constexpr int BM = 64, BN = 256, WM = 2, WN = 4, NW = 8, NTH = 512;
+  constexpr int WTM = BM / WM, WTN = BN / WN, TM = WTM / 16, TN = WTN / 16;
+  constexpr int RB = BN / 8 / NW;                  // 4 weight wave-instructions per stage (A: 1)
+  constexpr int PER = 1 + RB;
+  constexpr int STAGE = (BM + BN) * ROWB;          // 40 KiB
+  constexpr int NS = 4;
+  constexpr int LDS = NS * STAGE;
+  static_assert(LDS <= 160 * 1024 && det_lds(BM, BN) <= LDS, "LDS budget");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
+  unsigned char* es = smem;                        // zs + row table, after the K loop
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+  const int g = lane >> 4, li = lane & 15;
+  const int m0 = blockIdx.x * BM;
+  if (m0 >= p.M) return;
+  const int nk = p.kpad / BKE;
+  const auto xr = make_rsrc(p.x, p.xbytes);
+  const auto wr = make_rsrc(p.w, p.wbytes);
+  const int lr = lane >> 3;
+  const int c = (lane & 7) ^ lr;
+  uint32_t b_off[RB];
+#pragma unroll
+  for (int j = 0; j < RB; ++j) b_off[j] = (uint32_t)((((j * NW + wave) * 8 + lr) * p.kpad + c * 8) * 2);
+  const int hw = p.Ho * p.Wo;
+  uint32_t aoff = OOB;
+  {
+    const int m = m0 + wave * 8 + lr;
+    if (m < p.M) {
+      const int b = m / hw, cell = m - b * hw, ho = cell / p.Wo, wo = cell - ho * p.Wo;
+      aoff = (uint32_t)((pix_index(b, ho, wo, p.H, p.W) * p.xc + p.xoff + c * 8) * 2);
+    }
+  }
+  auto issue = [&](int k, int slot) __attribute__((always_inline)) {
+    unsigned char* As = smem + slot * STAGE;
+    unsigned char* Bs = As + BM * ROWB;
+    const uint32_t so = (uint32_t)k * BKE * 2;
+    dma16(xr, As + wave * 8 * ROWB, aoff, so);
+#pragma unroll
+    for (int j = 0; j < RB; ++j) dma16(wr, Bs + (j * NW + wave) * 8 * ROWB, b_off[j], so);
+    asm volatile("" ::: "memory");
+  };
+  f4 acc[TN][TM];
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int col = wn * WTN + j * 16 + g * 4;
+    f4 bv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) bv[e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) acc[j][i] = bv;
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // bias
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s)
+    if (s < nk) issue(s, s);
+  for (int k = 0; k < nk; ++k) {
+    ring_wait<PER, NS - 2>(nk - 1 - k);   // stage k landed; up to NS - 2 later stages in flight
+    __builtin_amdgcn_s_barrier();
+    if (k + NS - 1 < nk) issue(k + NS - 1, (k + NS - 1) & (NS - 1));   // into the slot step k - 1 read
+    const unsigned char* As = smem + (k & (NS - 1)) * STAGE;
+    const unsigned char* Bs = As + BM * ROWB;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const int ch = s * 4 + g;
+      u4 xa[TM], wb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) {
+        const int row = wm * WTM + i * 16 + li;
+        xa[i] = *reinterpret_cast<const u4*>(As + row * ROWB + swz(row, ch) * 16);
+      }
+#pragma unroll
+      for (int j = 0; j < TN; ++j) {
+        const int row = wn * WTN + j * 16 + li;
+        wb[j] = *reinterpret_cast<const u4*>(Bs + row * ROWB + swz(row, ch) * 16);
+      }
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          acc[j][i] = __builtin_amdgcn_mfma_f32_16x16x32_f16(__builtin_bit_cast(h8, wb[j]),
+                                                             __builtin_bit_cast(h8, xa[i]), acc[j][i], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();   // the ring is free: the staging image and row table take its place
+  if (tid < 8) det_tab_ptrs<BM, BN>(es).anc[tid] = p.anchor[tid];
+  det_table<BM, BN, NTH, false>(p, es, m0, tid);
+  {
+    constexpr int NO = 85, NA = 3;
+    float* zs = reinterpret_cast<float*>(es);
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int ch = wn * WTN + j * 16 + g * 4 + e;
+        const int ca = ch / NO;
+        const int zo = ca < NA ? ca * BM * NO + (ch - ca * NO) : NA * BM * NO;
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+          zs[zo + (zo < NA * BM * NO ? (wm * WTM + i * 16 + li) * NO : 0)] = det_sig(acc[j][i][e]);
+      }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const int mb = m0 / hw;
+  const long long zb = (long long)mb * p.nrows + p.row_off + (m0 - mb * hw);
+  const auto zr = make_rsrc(p.z + (size_t)zb * 85, 0x7fffffffu);
+  const auto br = make_rsrc(p.best ? p.best + (size_t)zb * 4 : p.z, 0x7fffffffu);
+  det_tail_fixed<BM, NTH>(p, es, tid, zr, br, zb);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
 
@@ -863,6 +999,13 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
       else if (rwd8 == 6) YV7_LAUNCH((conv_det_rw_kernel<16, 0, 6>), dim3(grid), dim3(512), 0, st, p);
       else YV7_LAUNCH((conv_det_rw_kernel<16, 0, 4>), dim3(grid), dim3(512), 0, st, p);
     }
+    return hipGetLastError();
+  }
+  // one 64-pixel tile per CU at most (yolov7 bs 32's P5 head): the one-tile head with its deep ring (round 6;
+  // YV7_DET_1T=0: off)
+  static const int one_tile = [] { const char* e = getenv("YV7_DET_1T"); return e ? atoi(e) : 1; }();
+  if (one_tile && p.variant == 0 && T <= cus && det_lds(64, 256) <= 4 * (64 + 256) * ROWB) {
+    YV7_LAUNCH(conv_det_1tile_kernel, dim3((unsigned)T), dim3(512), 0, st, p);
     return hipGetLastError();
   }
   if (p.variant == 98) YV7_LAUNCH(conv_det_pring_kernel<1>, dim3(grid), dim3(512), 0, st, p);
@@ -1137,19 +1280,6 @@ __device__ __forceinline__ bool splitk_reduce(const ConvParams& p, unsigned char
 #pragma unroll
     for (int i = 0; i < TM; ++i) acc[j][i] = sum[j][i];
   return true;
-}
-
-// vmcnt before ring step kt: stage kt landed, the min(MAXN, ahead) stages issued after it (PER DMA
-// instructions each) may stay in flight — an immediate per case
-template <int PER, int MAXN>
-__device__ __forceinline__ void ring_wait(int ahead) {
-  if constexpr (MAXN <= 0) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  } else {
-    static_assert(MAXN * PER <= 63, "vmcnt range");
-    if (ahead >= MAXN) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(MAXN * PER) : "memory");
-    else ring_wait<PER, MAXN - 1>(ahead);
-  }
 }
 
 // ---------------------------------------------------------------------------------------------
