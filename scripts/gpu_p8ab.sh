@@ -2,7 +2,7 @@
 # p8 issue A/B (round 6): convbench timings and the instruction-mix PMC pass of the
 # 8-phase ring on its yolov7 shapes, for the library built from the previous tree (libyv7_base.so) and this
 # tree's; the outputs land in gpurun_out/TAG/.
-# usage: bash scripts/gpu_p8ab.sh TAG
+# usage: [LIBS="base v1 cur"] bash scripts/gpu_p8ab.sh TAG   (libyv7_NAME.so each; cur = this tree's)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=$1
@@ -11,7 +11,8 @@ LIBD=$R/yolo-series_amd/yv7
 mkdir -p $O
 cp $LIBD/libyv7.so $LIBD/libyv7_cur.so || exit 1
 cd /tmp && export TMPDIR=/tmp
-for lib in base cur base cur; do
+LIBS=${LIBS:-base cur}
+for lib in $LIBS $LIBS; do
   cp $LIBD/libyv7_$lib.so $LIBD/libyv7.so || exit 1
   for shape in "1x1 1024->1024 @40" "1x1 2048->512 @20" "1x1 1024->1024 @20"; do
     f=$O/cb_${lib}_$(echo "$shape" | tr -cd '0-9a-z_').txt
@@ -19,7 +20,7 @@ for lib in base cur base cur; do
     grep -E "^ *variant|us" $f | tail -2
   done
 done
-for lib in base cur; do
+for lib in $LIBS; do
   cp $LIBD/libyv7_$lib.so $LIBD/libyv7.so || exit 1
   CB_SHAPE="1x1 1024->1024 @40" timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
     SQ_INSTS_VALU SQ_INSTS_MFMA SQ_INSTS_LDS SQ_INSTS_SALU SQ_INSTS_VMEM --output-format csv -d $O/pmc_$lib -o pmc \

@@ -1788,10 +1788,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
 
   // ---- staging cursors (A and B halves are staged in different phases, each in K-tile order)
-  int a_it = 0, a_kt = 0, b_it = 0, b_kt = 0, a_gk = 0, b_gk = 0;
+  int a_it = 0, a_kt = 0, b_it = 0, b_kt = 0;
   uint32_t a_off[2][AP], b_off[2][BP], a_so = 0;
   KWalk sa, sb;   // (!ONE) the A and B halves' chunk-major K walks (staged in different phases)
-  auto stage_a = [&](int h) {   // half h (0 / 1) of K-tile a_gk
+  auto stage_a = [&](int h, int par) {   // half h (0 / 1) of the next A K-tile, into buffer par
     if (h == 0) {
       if (a_kt == 0) {
         const int t = tile_at(a_it);
@@ -1806,16 +1806,15 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       a_so = ONE ? (uint32_t)a_kt * BKE * 2 : sa.a_offset(p);
       if (!ONE) sa.advance(p);
     }
-    unsigned char* d = smem + (a_gk & 1) * BUF + h * AHB;
+    unsigned char* d = smem + par * BUF + h * AHB;
 #pragma unroll
     for (int j = 0; j < AP; ++j) dma16(xr, d + (j * 8 + wave) * 8 * ROWB, a_off[h][j], a_so);
     if (h == 1) {
-      ++a_gk;
       if (++a_kt == nk) { a_kt = 0; ++a_it; }
     }
   };
   uint32_t b_so = 0;
-  auto stage_b = [&](int h) {   // half h of K-tile b_gk; staged B1 first, then B0
+  auto stage_b = [&](int h, int par) {   // half h of the next B K-tile into buffer par; B1 first, then B0
     if (h == 1) {
       if (b_kt == 0) {
         const int n0 = tile_at(b_it) % nN * BN;
@@ -1828,11 +1827,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
       b_so = ONE ? (uint32_t)b_kt * BKE * 2 : sb.b_offset(p);
       if (!ONE) sb.advance(p);
     }
-    unsigned char* d = smem + (b_gk & 1) * BUF + 2 * AHB + h * BHB;
+    unsigned char* d = smem + par * BUF + 2 * AHB + h * BHB;
 #pragma unroll
     for (int j = 0; j < BP; ++j) dma16(wr, d + (j * 8 + wave) * 8 * ROWB, b_off[h][j], b_so);
     if (h == 0) {
-      ++b_gk;
       if (++b_kt == nk) { b_kt = 0; ++b_it; }
     }
   };
@@ -1893,9 +1891,9 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
   };
 
   // ---- prologue: K-tile 0 whole, K-tile 1's A0, B1 and A1 in flight
-  stage_a(0); stage_b(1); stage_a(1); stage_b(0);
+  stage_a(0, 0); stage_b(1, 0); stage_a(1, 0); stage_b(0, 0);
   if (total > 1) {
-    stage_a(0); stage_b(1); stage_a(1);
+    stage_a(0, 1); stage_b(1, 1); stage_a(1, 1);
     asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1942,36 +1940,138 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8_kernel(const ConvParams p)
     __builtin_amdgcn_s_barrier();
   };
 
-  for (int k = 0; k < total; ++k) {
-    const unsigned char* bk = smem + (k & 1) * BUF;
-    const bool n1 = k + 1 < total, n2 = k + 2 < total;
+  // one K-tile: four phases over buffer par (K-tile k + 1's B0 and K-tile k + 2's A0, B1, A1 staged on
+  // the way when n1 / n2)
+  auto ktile = [&](auto par, bool n1, bool n2) __attribute__((always_inline)) {
+    const int P = par;   // a compile-time constant (integral_constant) or the K-tile's parity
+    const unsigned char* bk = smem + P * BUF;
     // phase 0: quadrant (0,0)
     read_b(bk + 2 * AHB);
     read_a(bk);
-    if (n1) stage_b(0);
+    if (n1) stage_b(0, P ^ 1);
     mfma_q(0, 0);
     // phase 1: (0,1)
     read_b(bk + 2 * AHB + BHB);
-    if (n2) stage_a(0);
+    if (n2) stage_a(0, P);
     mfma_q(0, 1);
     // phase 2: (1,1)
     read_a(bk + AHB);
-    if (n2) stage_b(1);
+    if (n2) stage_b(1, P);
     mfma_q(1, 1);
     // phase 3: (1,0); K-tile k+1 retired (k+2's A0, B1 and A1 may stay in flight)
     read_b(bk + 2 * AHB);
     if (n2) {
-      stage_a(1);
+      stage_a(1, P);
       asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     mfma_q(1, 0);
-    if (++ckt == nk) {
-      epilogue();
-      if (k != total - 1) {
-        ckt = 0;
-        init_tile(++ci);
+  };
+  // (ONE, nk even) the staging without cursors: the A / B halves' offsets for tile t (fresh_*), and one
+  // half's LDS-DMA at K offset so into buffer par
+  auto fresh_a = [&](int t) __attribute__((always_inline)) {
+    PixelWalk pw(p, (t / nN) * BM + wave * 8 + lr);
+#pragma unroll
+    for (int q = 0; q < 2 * AP; ++q) {
+      if (q) pw.advance(p, 64);
+      a_off[q / AP][q % AP] = a_origin(p, pw.b, pw.ho, pw.wo, c);
+    }
+  };
+  auto fresh_b = [&](int t) __attribute__((always_inline)) {
+    const int n0 = t % nN * BN;
+#pragma unroll
+    for (int q = 0; q < 2 * BP; ++q)
+      b_off[q / BP][q % BP] = (uint32_t)(((n0 + (q / BP) * BHR + ((q % BP) * 8 + wave) * 8 + lr) * p.kpad + c * 8) * 2);
+  };
+  auto dma_a = [&](int h, int par, uint32_t so) __attribute__((always_inline)) {
+    unsigned char* d = smem + par * BUF + h * AHB;
+#pragma unroll
+    for (int j = 0; j < AP; ++j) dma16(xr, d + (j * 8 + wave) * 8 * ROWB, a_off[h][j], so);
+  };
+  auto dma_b = [&](int h, int par, uint32_t so) __attribute__((always_inline)) {
+    unsigned char* d = smem + par * BUF + 2 * AHB + h * BHB;
+#pragma unroll
+    for (int j = 0; j < BP; ++j) dma16(wr, d + (j * 8 + wave) * 8 * ROWB, b_off[h][j], so);
+  };
+  // the same four phases, staging K-tile k + 1's B0 at so1 and K-tile k + 2's A0, B1, A1 at so2 (of tile t2,
+  // whose offsets are computed first when fresh2)
+  auto ktile_one = [&](auto par, bool n1, bool n2, uint32_t so1, uint32_t so2, bool fresh2, int t2)
+      __attribute__((always_inline)) {
+    constexpr int P = decltype(par)::value;
+    const unsigned char* bk = smem + P * BUF;
+    read_b(bk + 2 * AHB);
+    read_a(bk);
+    if (n1) dma_b(0, P ^ 1, so1);
+    mfma_q(0, 0);
+    read_b(bk + 2 * AHB + BHB);
+    if (n2) {
+      if (fresh2) fresh_a(t2);
+      dma_a(0, P, so2);
+    }
+    mfma_q(0, 1);
+    read_a(bk + AHB);
+    if (n2) {
+      if (fresh2) fresh_b(t2);
+      dma_b(1, P, so2);
+    }
+    mfma_q(1, 1);
+    read_b(bk + 2 * AHB);
+    if (n2) {
+      dma_a(1, P, so2);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(VMC) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    mfma_q(1, 0);
+  };
+  if (ONE && (nk & 1) == 0) {
+    // 1x1, nk even: the staging cursors follow from the compute cursor.  The pair (ckt, ckt + 1) stages
+    // K-tiles ckt + 1 .. ckt + 3; only ckt + 2 == nk moves the staging to the next tile, and then K-tile
+    // k + 2 (the even K-tile's A0 / B1 / A1) is that tile's first: its offsets are computed there, once.
+    for (int k = 0; k < total; k += 2) {
+      const bool more = k + 2 < total;
+      const bool wrap = ckt + 2 == nk;
+      const uint32_t s2 = wrap ? 0u : (uint32_t)(ckt + 2) * BKE * 2;
+      ktile_one(std::integral_constant<int, 0>{}, true, more, (uint32_t)(ckt + 1) * BKE * 2, s2, wrap,
+                wrap && more ? tile_at(ci + 1) : 0);
+      ktile_one(std::integral_constant<int, 1>{}, more, more, s2, s2 + BKE * 2, false, 0);
+      ckt += 2;
+      if (ckt == nk) {
+        epilogue();
+        if (more) {
+          ckt = 0;
+          init_tile(++ci);
+        }
+      }
+    }
+  } else if ((nk & 1) == 0) {
+    // nk even (round 6): every tile starts on an even K-tile, so two K-tiles per trip give each phase its
+    // buffer as a compile-time constant (the LDS read bases and DMA destinations are loop-invariant
+    // instead of recomputed from the K-tile's parity every phase), and only the odd K-tile can end a tile.
+    // total is even: n1 holds for the even K-tile, and k + 2 < total stands for the rest.
+    for (int k = 0; k < total; k += 2) {
+      const bool more = k + 2 < total;
+      ktile(std::integral_constant<int, 0>{}, true, more);
+      ktile(std::integral_constant<int, 1>{}, more, more);
+      ckt += 2;
+      if (ckt == nk) {
+        epilogue();
+        if (more) {
+          ckt = 0;
+          init_tile(++ci);
+        }
+      }
+    }
+  } else {
+    for (int k = 0; k < total; ++k) {
+      ktile(k & 1, k + 1 < total, k + 2 < total);
+      if (++ckt == nk) {
+        epilogue();
+        if (k != total - 1) {
+          ckt = 0;
+          init_tile(++ci);
+        }
       }
     }
   }
