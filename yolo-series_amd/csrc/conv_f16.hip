@@ -2126,10 +2126,10 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
   for (int i = tid; i < p.cout; i += NTH) bias_l[i] = p.bias[i];
 
   // ---- staging cursor: K-tile s_gk, half h = A half h + B half h
-  int s_it = 0, s_kt = 0, s_gk = 0;
+  int s_it = 0, s_kt = 0;
   uint32_t a_off[2][2], b_off[2], a_so = 0, b_so = 0;
   KWalk su;
-  auto stage = [&](int h) {
+  auto stage = [&](int h, int par) {   // half h of the next K-tile into buffer par
     if (h == 0) {
       if (s_kt == 0) {
         const int t = tw.at(s_it);
@@ -2148,12 +2148,11 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
       b_so = ONE ? (uint32_t)s_kt * BKE * 2 : su.b_offset(p);
       if (!ONE) su.advance(p);
     }
-    unsigned char* d = smem + (s_gk % 3) * BUF;
+    unsigned char* d = smem + par * BUF;
 #pragma unroll
     for (int j = 0; j < 2; ++j) dma16(xr, d + h * AH + (j * 8 + wave) * 8 * ROWB, a_off[h][j], a_so);
     dma16(wr, d + 2 * AH + h * BH + wave * 8 * ROWB, b_off[h], b_so);
     if (h == 1) {
-      ++s_gk;
       if (++s_kt == nk) { s_kt = 0; ++s_it; }
     }
   };
@@ -2209,9 +2208,9 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
   };
 
   // ---- prologue: K-tiles 0 and 1 staged, 0 retired
-  stage(0); stage(1);
+  stage(0, 0); stage(1, 0);
   if (total > 1) {
-    stage(0); stage(1);
+    stage(0, 1); stage(1, 1);
     asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -2247,10 +2246,11 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
       }
   };
 
-  int ci = 0, ckt = 0;
-  for (int k = 0; k < total; ++k) {
-    const unsigned char* bk = smem + (k % 3) * BUF;
-    const bool n2 = k + 2 < total;
+  // one K-tile over buffer par (K-tile k + 2 staged on the way into buffer (par + 2) % 3 when n2)
+  auto ktile = [&](auto par, bool n2) __attribute__((always_inline)) {
+    const int P = par;   // a compile-time constant (integral_constant) or k % 3
+    const unsigned char* bk = smem + P * BUF;
+    const int P2 = P == 0 ? 2 : P - 1;
     // phase 0: the wave's whole B part (kept for phase 1) + A half 0
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb)
@@ -2260,21 +2260,42 @@ __global__ __launch_bounds__(512, 1) void conv_f16_p8n_kernel(const ConvParams p
         wb[sb][j] = *reinterpret_cast<const u4*>(bk + 2 * AH + wn * BH + row * ROWB + swz(row, sb * 4 + g) * 16);
       }
     read_a(bk);
-    if (n2) stage(0);
+    if (n2) stage(0, P2);
     mfma_h(0);
     // phase 1: A half 1; K-tile k+1 retired (k+2 may stay in flight)
     read_a(bk + AH);
     if (n2) {
-      stage(1);
+      stage(1, P2);
       asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     }
     mfma_h(1);
-    if (++ckt == nk) {
-      epilogue();
-      ckt = 0;
-      if (++ci < ntl) init_tile(ci);
+  };
+  int ci = 0, ckt = 0;
+  if (nk % 3 == 0) {
+    // nk a multiple of 3 (every 3x3 layer here: nk = 9 cin / 64; round 6): every tile starts on a K-tile
+    // k = 0 mod 3, so three K-tiles per trip give each its buffer as a compile-time constant, and only the
+    // third can end a tile
+    for (int k = 0; k < total; k += 3) {
+      ktile(std::integral_constant<int, 0>{}, k + 2 < total);
+      ktile(std::integral_constant<int, 1>{}, k + 3 < total);
+      ktile(std::integral_constant<int, 2>{}, k + 4 < total);
+      ckt += 3;
+      if (ckt == nk) {
+        epilogue();
+        ckt = 0;
+        if (++ci < ntl) init_tile(ci);
+      }
+    }
+  } else {
+    for (int k = 0; k < total; ++k) {
+      ktile(k % 3, k + 2 < total);
+      if (++ckt == nk) {
+        epilogue();
+        ckt = 0;
+        if (++ci < ntl) init_tile(ci);
+      }
     }
   }
   if (grp == 0) __builtin_amdgcn_s_barrier();
