@@ -168,13 +168,23 @@ __global__ __launch_bounds__(64 * NWV, 1) void conv3x3_ws64_kernel(const ConvPar
   // serves all three tap rows.  The next super-step's 18 fragments are read into the other register
   // set before this one's MFMAs, so LDS latency hides under 768 MFMA cycles; `side(ss)` runs after
   // super-step ss's MFMAs are issued (the previous tile's epilogue rides there).
+  // (round 6) one opaque LDS offset per (tap column, K half): the taps' rows and fragments then sit within
+  // the read's 16-bit offset field (r * 3 * WTAP + j * 2 KiB <= 54 KiB) instead of costing a v_or each
+  uint32_t wcol[3][2];
+#pragma unroll
+  for (int sc = 0; sc < 3; ++sc)
+#pragma unroll
+    for (int sub = 0; sub < 2; ++sub) {
+      wcol[sc][sub] = (uint32_t)(2 * PBUF + sc * WTAP) + wbase[sub];
+      asm volatile("" : "+v"(wcol[sc][sub]));
+    }
   auto load_w = [&](int ss, u4 (&wf)[3][4]) __attribute__((always_inline)) {
     const int sc = ss >> 1, sub = ss & 1;
 #pragma unroll
     for (int r = 0; r < 3; ++r)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
-        wf[r][j] = *reinterpret_cast<const u4*>(wl + (r * 3 + sc) * WTAP + j * 16 * 128 + wbase[sub]);
+        wf[r][j] = *reinterpret_cast<const u4*>(smem + wcol[sc][sub] + (r * 3 * WTAP + j * 16 * 128));
   };
   auto load_x = [&](const unsigned char* pb, int ss, u4 (&xf)[NX]) __attribute__((always_inline)) {
     const int sc = ss >> 1, sub = ss & 1;
