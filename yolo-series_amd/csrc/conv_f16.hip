@@ -801,16 +801,22 @@ __global__ __launch_bounds__(512, 1) void conv_det_1tile_kernel(const ConvParams
 // its K loop.  Stage s is read at global step s; the stores of the epilogue between two tiles are younger
 // than the stages issued before it, so the counted wait at step k of a tile allows D - 1 younger stages,
 // plus the previous epilogue's nst stores while those stages were issued before it (k < D, tile > 0).
-template <int NCH, int HOOK = 0, int D = 0>
+// BM (round 6): pixels per tile, 64 or 32 — at 32 the four pixel pieces of a stage are issued by waves 0-3 and
+// again by waves 4-7 (the same bytes to the same rows), so every wave's counted waits stay the same.
+template <int NCH, int HOOK = 0, int D = 0, int BM = 64>
 __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p) {
-  constexpr int BM = 64, BN = 256, NTH = 512, TM = 4, TN = 2, NK = NCH / 2;
+  constexpr int BN = 256, NTH = 512, TM = BM / 16, TN = 2, NK = NCH / 2;
+  static_assert(BM == 64 || BM == 32, "tile");
+  // epilogue stores per wave per tile (det_tail_fixed): row records, z rows
+  constexpr int NREC = (BM * 3 * 4 + NTH - 1) / NTH, NZS = (3 * (BM / 4) + NTH / 85 - 1) / (NTH / 85);
+  constexpr int NSTB = NREC + NZS, NSTN = NZS;
   constexpr int PER = HOOK == 1 ? 0 : 1;           // one A piece per wave per stage
   constexpr int STAGE = BM * ROWB;                 // 8 KiB
   constexpr int R = D > 0 ? D + 1 : 2;             // ring slots
   constexpr int RING = R * STAGE;
   constexpr int LDS = RING + det_lds(BM, BN);
   static_assert(LDS <= 160 * 1024, "LDS budget");
-  static_assert(D == 0 || ((D - 1) * PER + 10 <= 63 && D <= NK), "counted waits");
+  static_assert(D == 0 || ((D - 1) * PER + NSTB <= 63 && D <= NK), "counted waits");
   constexpr int NO = 85, NA = 3;
   __shared__ __attribute__((aligned(16))) unsigned char smem[LDS];
   unsigned char* es = smem + RING;                 // zs + row table
@@ -839,7 +845,7 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
   const int hw = p.Ho * p.Wo;
   auto a_off = [&](int it) -> uint32_t {
     if (it >= ntl) return OOB;
-    const int m = tw.at(it) * BM + wave * 8 + lr;
+    const int m = tw.at(it) * BM + (wave % (BM / 8)) * 8 + lr;
     if (m >= p.M) return OOB;
     const int b = m / hw, cell = m - b * hw, ho = cell / p.Wo, wo = cell - ho * p.Wo;
     return (uint32_t)((pix_index(b, ho, wo, p.H, p.W) * p.xc + p.xoff + c8 * 8) * 2);
@@ -848,7 +854,7 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
   int i_it = 0, i_k = 0, i_slot = 0;
   uint32_t i_aoff = a_off(0);
   auto issue = [&]() __attribute__((always_inline)) {
-    if constexpr (HOOK != 1) dma16(xr, smem + i_slot * STAGE + wave * 8 * ROWB, i_aoff, (uint32_t)i_k * BKE * 2);
+    if constexpr (HOOK != 1) dma16(xr, smem + i_slot * STAGE + (wave % (BM / 8)) * 8 * ROWB, i_aoff, (uint32_t)i_k * BKE * 2);
     asm volatile("" ::: "memory");
     if (++i_slot == R) i_slot = 0;
     if (++i_k == NK) {
@@ -865,7 +871,7 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
 #pragma unroll
     for (int e = 0; e < 4; ++e) bv[j][e] = col + e < p.cout ? p.bias[col + e] : 0.0f;
   }
-  const int nst = p.best ? 10 : 8;   // epilogue stores per wave per tile (det_tail_fixed)
+  const int nst = p.best ? NSTB : NSTN;
   // z slot of each of this lane's 8 channels (the padding channel 255 -> a spare slot)
   int zo[TN][4];
 #pragma unroll
@@ -894,19 +900,19 @@ __global__ __launch_bounds__(512, 1) void conv_det_rw_kernel(const ConvParams p)
         // stage (it, k) landed: younger are stage (it, 1) and the previous epilogue's stores at k = 0, the
         // previous epilogue's stores at k = 1 (both stages of a tile start are issued before them)
         if (k == 0) {
-          if (it > 0 && nst == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 10) : "memory");
-          else if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + 8) : "memory");
+          if (it > 0 && nst == NSTB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + NSTB) : "memory");
+          else if (it > 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER + NSTN) : "memory");
           else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(PER) : "memory");
         } else if (k == 1 && it > 0) {
-          if (nst == 10) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-          else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+          if (nst == NSTB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTB) : "memory");
+          else asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NSTN) : "memory");
         } else {
           asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         }
       } else {
         if (k >= D || it == 0) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * PER) : "memory");
-        else if (nst == 10) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * PER + 10) : "memory");
-        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * PER + 8) : "memory");
+        else if (nst == NSTB) asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * PER + NSTB) : "memory");
+        else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((D - 1) * PER + NSTN) : "memory");
       }
       __builtin_amdgcn_s_barrier();
       if (D > 0 || k >= 1) issue();     // D > 0: stage s + D; D = 0: stage (it, k + 1) or the next tile's first
@@ -989,6 +995,19 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
     }
     // YV7_DET_RWD: pixel stages in flight (conv_det_rw_kernel's D; 0 = the round-5 two-slot schedule)
     static const int rwd = [] { const char* e = getenv("YV7_DET_RWD"); return e ? atoi(e) : 4; }();
+    // 32-pixel tiles at K = 512 (round 6): 1x1 512->255 @40 at bs 32 is 800 tiles of 64 = 4 rounds on 200
+    // blocks, or 1600 of 32 = 7 half-size rounds on 229 — 33.7 -> 31.5 us in-network, same box; at K = 256
+    // (256->255 @80, 3200 / 6400 tiles) the halved tiles lose, 60.6 -> 70.0 (profiles/r6_det/bm32/).
+    // YV7_DET_BM=32 / 64 forces either.
+    static const int bm_env = [] { const char* e = getenv("YV7_DET_BM"); return e ? atoi(e) : 0; }();
+    const int bm = bm_env ? bm_env : (p.kpad == 512 ? 32 : 64);
+    if (bm == 32 && rwd == 4) {
+      const long T2 = (p.M + 31) / 32, per2 = (T2 + cus - 1) / cus;
+      const int grid2 = (int)((T2 + per2 - 1) / per2);
+      if (p.kpad == 256) YV7_LAUNCH((conv_det_rw_kernel<8, 0, 4, 32>), dim3(grid2), dim3(512), 0, st, p);
+      else YV7_LAUNCH((conv_det_rw_kernel<16, 0, 4, 32>), dim3(grid2), dim3(512), 0, st, p);
+      return hipGetLastError();
+    }
     if (p.kpad == 256) {
       if (rwd == 0) YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
       else YV7_LAUNCH((conv_det_rw_kernel<8, 0, 4>), dim3(grid), dim3(512), 0, st, p);
