@@ -64,7 +64,7 @@ def parse(argv=None):
                     'kernel-boundary gaps of one stream with the other\'s work)')
     ap.add_argument('--no-pipeline', action='store_true', help='run each batch\'s NMS (+ detection all-gather) '
                     'on the forward\'s stream instead of overlapping it with the next batch\'s forward')
-    ap.add_argument('--streams', type=int, default=3, help='batches in flight (measured on MI355X, bs32 yolov7: 1 -> 5.6k, 2 -> 6.2k, 3 -> 6.3k, 4 -> 6.1k img/s): batch k runs its forward + NMS on '
+    ap.add_argument('--streams', type=int, default=3, help='batches in flight (MI355X, bs32 yolov7, round-6 kernels, profiles/r6_streams/: 2 -> 7.93k, 3 -> 7.93k, 4 -> 7.70k img/s): batch k runs its forward + NMS on '
                     'HIP stream k %% S with its own workspace and buffers, so consecutive batches overlap')
     ap.add_argument('--prio', default='', help='comma-separated HIP stream priorities of the --streams streams '
                     '(measured: default 6.38k, -1,0,0 6.34k, -1,-1,0 6.23k img/s — equal priorities pack best)')
