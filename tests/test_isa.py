@@ -99,3 +99,34 @@ def test_early_read_detector():
     lines = ['buffer_load_dwordx4 v[4:7], v1, s[0:3], 0 offen', 'v_mov_b32 v8, v9', 's_waitcnt vmcnt(0)',
              'v_mov_b32 v8, v5']
     assert not I.early_async_reads(lines, {0})
+
+
+def ws64_wide_ors(asm):
+    """Per conv3x3_ws64_kernel instantiation: the v_or_b32 with a constant of 64 KiB or more (an LDS address
+    past the ds_read offset field, built per read instead of folded into the offset)."""
+    return {n: sum(1 for ln in lines if re.match(r'v_or_b32_e32 v\d+, 0x[0-9a-f]{5,}', ln))
+            for n, (lines, _) in I.functions(asm).items() if 'conv3x3_ws64_kernel' in n}
+
+
+def test_ws64_weight_reads_fold_their_offsets(asm_dir):
+    """Round 6 (profiles/r6_ws64/): the weight reads of the 8-wave ws64 kernel take one opaque
+    base per (tap column, K half) and carry the tap / fragment offsets in the ds_read offset field; the
+    compiler's `base | constant` form cost a v_or per read (114 in the 8-wave kernel) and 42 VGPRs."""
+    ors = ws64_wide_ors(I.device_asm(os.path.join(I.CSRC, 'conv_ws.hip'), str(asm_dir / 'ws.s')))
+    eight = {n: c for n, c in ors.items() if n.endswith('ELi8EEEvNS_10ConvParamsE')}
+    assert eight and all(c <= 16 for c in eight.values()), eight
+
+
+def test_ws64_check_catches_the_per_read_ors(asm_dir):
+    """Negative control: the round-5 source (before commit 1aba2fd) builds its weight addresses per read."""
+    if not shutil.which('git') or not os.path.isdir(os.path.join(ROOT, '.git')):
+        pytest.skip('no git history')
+    r = subprocess.run(['git', '-C', ROOT, 'show', '1aba2fd~1:yolo-series_amd/csrc/conv_ws.hip'],
+                       capture_output=True, text=True)
+    if r.returncode:
+        pytest.skip('commit 1aba2fd not in this history')
+    src = asm_dir / 'conv_ws_before.hip'
+    src.write_text(r.stdout)
+    ors = ws64_wide_ors(I.device_asm(str(src), str(asm_dir / 'ws_before.s')))
+    eight = {n: c for n, c in ors.items() if n.endswith('ELi8EEEvNS_10ConvParamsE')}
+    assert eight and all(c > 60 for c in eight.values()), eight
