@@ -2585,7 +2585,9 @@ int lr_default_cfg(const ConvParams& p) {
     // Round 5 (profiles/r5_misc/tune_small_w6.txt, us): 160 x 64 from 480 such tiles (w6 bs 8 384->384 @40
     // 38.0 / 37.9 / 37.1 / 37.3 -> 35.6-35.9); 64-pixel tiles on the 3 200-pixel layers (w6 bs 8 @20:
     // 512->512 25.3 / 25.0 / 25.2 -> 23.7-24.1, 512->256 18.4 -> 17.1, 256->256 11.3 -> 10.4)
-    if (cfg == 1 && p.M <= 6400 && lr_supported(p, 3)) cfg = 3;
+    // (round 6, profiles/r6_tune/tune_w6_all.txt: not for cout 1024 — w6 bs 8 512->1024 @20 42.2 -> 36.9 us on
+    // the 128-pixel tiles)
+    if (cfg == 1 && p.M <= 6400 && p.cout <= 512 && lr_supported(p, 3)) cfg = 3;
     if (lr_supported(p, cfg)) return cfg;
   }
   return -1;
