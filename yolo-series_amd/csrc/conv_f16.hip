@@ -1011,11 +1011,8 @@ hipError_t launch_det_pring(const ConvParams& p, int cus, hipStream_t st) {
     if (p.kpad == 256) {
       if (rwd == 0) YV7_LAUNCH(conv_det_rw_kernel<8>, dim3(grid), dim3(512), 0, st, p);
       else YV7_LAUNCH((conv_det_rw_kernel<8, 0, 4>), dim3(grid), dim3(512), 0, st, p);
-    } else {   // K = 512: 8 K steps, so up to 8 stages may run ahead (YV7_DET_RWD8: 4 / 6 / 8)
-      static const int rwd8 = [] { const char* e = getenv("YV7_DET_RWD8"); return e ? atoi(e) : 4; }();
+    } else {   // K = 512 (6 and 8 stages ahead measured no faster than 4: profiles/r6_det/ring_k512/)
       if (rwd == 0) YV7_LAUNCH(conv_det_rw_kernel<16>, dim3(grid), dim3(512), 0, st, p);
-      else if (rwd8 == 8) YV7_LAUNCH((conv_det_rw_kernel<16, 0, 8>), dim3(grid), dim3(512), 0, st, p);
-      else if (rwd8 == 6) YV7_LAUNCH((conv_det_rw_kernel<16, 0, 6>), dim3(grid), dim3(512), 0, st, p);
       else YV7_LAUNCH((conv_det_rw_kernel<16, 0, 4>), dim3(grid), dim3(512), 0, st, p);
     }
     return hipGetLastError();
