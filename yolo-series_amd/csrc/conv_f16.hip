@@ -2577,7 +2577,9 @@ int lr_default_cfg(const ConvParams& p) {
     if (p.H % 10 == 0) {
       const long g10 = (long)((p.B + 3) / 4) * (p.H / 10) * (p.W / 4);
       if (p.cout % 128 == 0 && p.cout >= 2 * p.cin && p.cin <= 384 && g10 * (p.cout / 128) >= 400) cfg = 5;
-      else if (p.cout != 128 && p.cout % 64 == 0 && g10 * (p.cout / 64) >= 480) cfg = 6;
+      // (round 6: the 128-output exclusion kept only for 128-input layers — 256->128 took 160 x 64 by 1-2 us in
+      // every sweep: yolov7 @40 ops 49 / 66, w6 @80 ops 57 / 73, profiles/r6_tune/tune_{yolov7,w6}_all.txt)
+      else if ((p.cout != 128 || p.cin >= 256) && p.cout % 64 == 0 && g10 * (p.cout / 64) >= 480) cfg = 6;
     }
     // Round 5 (profiles/r5_misc/tune_small_w6.txt, us): 160 x 64 from 480 such tiles (w6 bs 8 384->384 @40
     // 38.0 / 37.9 / 37.1 / 37.3 -> 35.6-35.9); 64-pixel tiles on the 3 200-pixel layers (w6 bs 8 @20:
