@@ -243,6 +243,7 @@ int find_chain(const yv7_plan* p, size_t i, int B, int H, int W, const std::vect
       if (q.Ho != (H >> to.shift) || q.Wo != (W >> to.shift)) ok = false;
       int cfg = yv7::lr_default_cfg(q);
       if (cfg == 0 || cfg == 2) ++cfg;   // 128-channel tiles -> 64-channel (conv_lr.hip CHAIN_FORMS)
+      if (cfg == 5 || cfg == 6) cfg = 1;  // 160-pixel tiles (H % 10 == 0) -> the 80-pixel 64-channel form
       if (cfg < 0 || (j > 1 && cfg != c->cfg1)) ok = false;
       if (j == 0) c->cfg0 = cfg;
       if (j == 1) c->cfg1 = cfg;
